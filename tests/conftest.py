@@ -1,0 +1,28 @@
+"""Shared pytest setup: registers the `gpu` marker and puts the product package
+directory (multigrid-feanet_amd/) and the oracle on sys.path."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "multigrid-feanet_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device) and the built libfeanet_hip.so")
+
+
+def golden(name):
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def gold():
+    return golden
