@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: DoF-updates/s per V-cycle (fp64) + achieved HBM GB/s, 4097^2 Poisson (BASELINE.json).
+
+One "step" = one full V-cycle (12 levels, V(1,1), the reference's MultiGrid.Step schedule) of the
+fused HIP kernels on a 4097 x 4097 fp64 Poisson problem resident in HBM (synthetic seeded
+right-hand side, zero initial guess), replayed as a HIP graph.  value = B * N^2 * ranks / t_step.
+
+Also reported on the same JSON line:
+  roofline      the dominant kernel (fine-level Ke-stencil Jacobi sweep, fea_mg_sweep at 4097^2):
+                algorithmic bytes per launch (24 B per interior node: read u, read f, write u')
+                / its average duration from HIP events on its stream, vs the 8 TB/s HBM peak;
+                `traffic` = measured HBM bytes per launch from rocprofv3 PMC (profiles/, if present)
+  cpu_baseline  the CPU oracle (numpy restatement of the reference V-cycle, 1 thread) on the same
+                workload, a bounded sample of whole V-cycles, rank 0 at N = 1 only.
+
+Multi-GPU (torchrun, one process per GPU): each rank runs its own 4097^2 problem (weak scaling,
+replicas; the domain-decomposed 8193^2 path is bench --config dd8193).  Timing: barrier +
+synchronize on both sides of the K steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multigrid-feanet_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "DoF-updates/sec per V-cycle (fp64) + achieved HBM GB/s, 4097² Poisson"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_init():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        torch.cuda.set_device(local)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, ws):
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def time_dominant_kernel(s, reps):
+    """Average duration of the fine-level Jacobi sweep (fea_mg_sweep, 4097^2) from HIP events
+    recorded on the stream the kernel is launched on."""
+    from feanet_amd import _lib
+    L0 = s.levels[0]
+    stream = torch.cuda.current_stream()
+    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab,
+            L0.B, L0.N, L0.ld, L0.bs, stream.cuda_stream)
+    for _ in range(3):
+        _lib.call("mg_sweep", s.dtype, *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        _lib.call("mg_sweep", s.dtype, *args)
+    e1.record(stream)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    nodes = L0.B * (L0.N - 2) ** 2
+    bytes_per_launch = 24 * nodes  # read u, read f, write u' (fp64)
+    return t, bytes_per_launch
+
+
+def load_traffic(kernel_key):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    try:
+        d = json.load(open(p))
+        rec = d.get(kernel_key)
+        return (rec["hbm_bytes_per_launch"], rec.get("source")) if rec else (None, None)
+    except Exception:
+        return None, None
+
+
+def cpu_baseline(n, seconds_budget=20.0):
+    """Oracle (numpy, single thread) V-cycles on the same 4097^2 fp64 Poisson workload."""
+    from oracle import feanet_oracle as orc
+    rng = np.random.default_rng(0)
+    N = n + 1
+    f = rng.standard_normal((1, N, N))
+    mg = orc.OracleMultigrid(n, "poisson", np.float64)
+    v = np.zeros((1, N, N))
+    t0 = time.perf_counter()
+    v = mg.step(v, f)  # warm-up cycle (page-in, allocation)
+    t1 = time.perf_counter()
+    first = t1 - t0
+    k = max(1, min(5, int(seconds_budget / max(first, 1e-3)) - 1))
+    times = []
+    for _ in range(k):
+        t0 = time.perf_counter()
+        v = mg.step(v, f)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": N * N / t, "unit": "DoF-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{k} timed V-cycles (median {t:.2f} s, +1 warm-up) of the {N}x{N} fp64 Poisson V(1,1) "
+                      f"workload by the numpy oracle (oracle/feanet_oracle.py), 1 thread, host of the GPU box"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=4096, help="intervals per edge (N = n+1 nodes)")
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--problem", default="poisson", choices=["poisson", "interface"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    args = ap.parse_args()
+
+    ws, rank = dist_init()
+    from feanet_amd.solver import MultigridSolver
+    T = torch.float64 if args.dtype == "f64" else torch.float32
+    n, B = args.n, args.batch
+    N = n + 1
+    s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
+    s.load()
+    r0 = s.residual_norm()
+
+    for _ in range(args.warmup):
+        s.vcycle()
+    torch.cuda.synchronize()
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(args.steps)
+    torch.cuda.synchronize()
+    barrier(ws)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    t = max_over_ranks(t, ws)
+    rK = s.residual_norm()
+    ms_step = t / args.steps * 1e3
+    dof = B * N * N * ws
+    value = dof / (t / args.steps)
+    cycles = args.warmup + args.steps
+    conv = float((rK.max() / r0.max()).item()) ** (1.0 / cycles)
+
+    kt, kbytes = time_dominant_kernel(s, args.kernel_reps)
+    kt = max_over_ranks(kt, ws)
+    achieved = kbytes / kt / 1e9
+    traffic, tsrc = load_traffic("mg_sweep_f64_4097")
+    vbytes = s.bytes_per_vcycle()
+
+    rec = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "DoF-updates/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded Gaussian rhs, zero initial guess)",
+        "config": {"workload": f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) "
+                               f"(MultiGrid.Step semantics), batch {B} per GPU",
+                   "nodes_per_edge": N, "batch": B, "levels": s.L,
+                   "parallelism": "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "fea_mg_sweep (fine-level Ke-stencil Jacobi sweep, 4097^2 fp64)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": kt * 1e6,
+                     "algorithmic_bytes_per_launch": kbytes},
+        "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if ws == 1 else None,
+        "vcycle_algorithmic_bytes": vbytes,
+        "residual_contraction_per_cycle": conv,
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.problem == "poisson" and B == 1:
+        log("[bench] timing the CPU oracle baseline ...")
+        rec["cpu_baseline"] = cpu_baseline(n)
+    elif rank == 0:
+        rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

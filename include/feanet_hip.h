@@ -1,0 +1,191 @@
+/*
+ * feanet_hip.h — C ABI of libfeanet_hip.so, the MI355X (gfx950) kernels of the
+ * FEANet geometric-multigrid hot path.
+ *
+ * The reference (longfish/Multigrid-FEANet) has no native code: its hot path is
+ * PyTorch-CPU conv2d / conv_transpose2d inside nn.Modules.  Each entry point below
+ * replaces one of those module methods; the reference interface it stands in for is
+ * cited per function.  Python binds them with ctypes (feanet_amd/_lib.py); the
+ * reference-side binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - T is float (suffix _f32) or double (suffix _f64); arithmetic stays in T.
+ *  - All data pointers are DEVICE pointers owned by the caller; calls are
+ *    asynchronous on `stream` (a hipStream_t passed as void*; NULL = default).
+ *  - Return value: 0 on success, FEA_EINVAL (-1) for invalid arguments (nothing is
+ *    launched), otherwise the hipError_t of the launch.  No exception crosses the ABI.
+ *  - Functions are stateless and re-entrant; they never allocate or synchronise,
+ *    so they are safe inside hipGraph stream capture.
+ *  - Stencil tables: `ktab` = ntab x 9 coefficients (row-major 3x3, cross-correlation
+ *    orientation, ktab[p*9 + 3*dr + dc] multiplies u[r+dr-1][c+dc-1]); `omd` = ntab
+ *    values omega/d_p (d_p = ktab[p*9+4]); `pid` = uint8 pattern id per node (NULL:
+ *    every node uses pattern 0).  ntab <= FEA_MAX_PATTERNS.
+ *
+ * Two families:
+ *  (1) "Generic" ops on contiguous NCHW tensors [B, C, H, W] — the drop-in operator
+ *      boundary used by the FEANet.* shim modules (KNet/FNet/JacobiBlock/MultiGrid).
+ *  (2) "mg" ops on FRAMED level buffers owned by the MultigridSolver: node (r, c)
+ *      of sample b lives at  base[b*bstride + (r+1)*ld + (A-1) + c],  A = 128/sizeof(T)
+ *      (so column 1 starts a 128-byte line), with a zero ghost ring at r,c = -1 and N.
+ *      Use fea_mg_layout() for ld / bstride.  Boundary nodes hold the Dirichlet values
+ *      and are never written by mg kernels (SURVEY §8a A9 invariant).
+ */
+#ifndef FEANET_HIP_H
+#define FEANET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEA_EINVAL (-1)
+#define FEA_MAX_PATTERNS 16
+
+/* ---------------------------------------------------------------------------
+ * Library / layout queries
+ * ------------------------------------------------------------------------- */
+/* ABI version (bumped on any signature change). */
+int fea_abi_version(void);
+
+/* Framed layout of an N x N level for elements of `elem_size` bytes (4 or 8):
+ * writes the row pitch (elements) and the per-sample stride (elements).
+ * Returns 0, or FEA_EINVAL for unsupported N / elem_size. */
+int fea_mg_layout(int N, int elem_size, int* ld, long long* bstride);
+
+/* Bytes of double workspace needed by the norm kernels for this shape. */
+size_t fea_norm_workspace_bytes(int B, int N);
+
+/* ---------------------------------------------------------------------------
+ * (1) Generic ops, contiguous [B, C, H, W]
+ * ------------------------------------------------------------------------- */
+
+/* y = K u: y[i] = sum_d ktab[pid(i+d)][d] * u[i+d], zero padding.
+ * Replaces KNet.forward (FEANet/model.py:22-30); with ntab=1, pid=NULL it is FNet.forward
+ * (model.py:60-61) and one HNet layer (M-FEANet-mg_test.ipynb:104-106) too.  pid is [H, W]. */
+int fea_knet_apply_f32(const float* u, float* y, const uint8_t* pid, const float* ktab, int ntab,
+                       int B, int H, int W, void* stream);
+int fea_knet_apply_f64(const double* u, double* y, const uint8_t* pid, const double* ktab, int ntab,
+                       int B, int H, int W, void* stream);
+
+/* xs[b, p] = (pid == p) ? x[b] : 0, p < C.  Replaces KNet.split_x (model.py:37-47). */
+int fea_split_x_f32(const float* x, float* xs, const uint8_t* pid, int C, int B, int H, int W, void* stream);
+int fea_split_x_f64(const double* x, double* xs, const uint8_t* pid, int C, int B, int H, int W, void* stream);
+
+/* One weighted-Jacobi sweep, out-of-place:
+ *   u0 = u*geo + bc; r = f - K u0; out = (omd[pid]*r + u0)*geo + bc.
+ * geo/bc: NULL = square domain (1 inside, 0 on the edge) / zero; *_bstride = elements
+ * between samples (0 = broadcast).  Replaces JacobiBlock.jacobi_convolution
+ * (FEANet/jacobi.py:39-47) with reset_boundary (:27-29) fused in. */
+int fea_jacobi_sweep_f32(const float* u, const float* f, float* out, const uint8_t* pid,
+                         const float* ktab, const float* omd, int ntab,
+                         const float* geo, long long geo_bstride, const float* bc, long long bc_bstride,
+                         int B, int H, int W, void* stream);
+int fea_jacobi_sweep_f64(const double* u, const double* f, double* out, const uint8_t* pid,
+                         const double* ktab, const double* omd, int ntab,
+                         const double* geo, long long geo_bstride, const double* bc, long long bc_bstride,
+                         int B, int H, int W, void* stream);
+
+/* r = f - K u (the residual every driver forms, e.g. FEANet/multigrid.py:168). */
+int fea_residual_f32(const float* u, const float* f, float* r, const uint8_t* pid, const float* ktab,
+                     int ntab, int B, int H, int W, void* stream);
+int fea_residual_f64(const double* u, const double* f, double* r, const uint8_t* pid, const double* ktab,
+                     int ntab, int B, int H, int W, void* stream);
+
+/* Restriction, H = W = 2^k + 1 fine nodes -> Hc = (H+1)/2:
+ *   fc = w0 * pad0( conv2d(x[..., 1:-1, 1:-1], rtab, stride 2) ).
+ * C > 1: x is the split field [B, C, H, W], rtab holds C channel kernels (pid ignored).
+ * C == 1: x is [B, 1, H, W] and the kernel of each fine node is rtab[pid(node)].
+ * Replaces RestrictionNet.forward + MultiGrid.Restrict (FEANet/multigrid.py:50-60,115-122)
+ * and the mg_test / MM notebook Restrict methods. */
+int fea_restrict_f32(const float* x, int C, float* fc, const uint8_t* pid, const float* rtab, int ntab,
+                     float w0, int B, int H, int W, void* stream);
+int fea_restrict_f64(const double* x, int C, double* fc, const uint8_t* pid, const double* rtab, int ntab,
+                     double w0, int B, int H, int W, void* stream);
+
+/* Prolongation, coarse Hc x Wc -> fine (2Hc-1) x (2Wc-1):
+ *   out = add + w1 * conv_transpose2d(e, ptab, stride 2, padding 1)      (add may be NULL)
+ * C > 1: e is split [B, C, Hc, Wc]; C == 1: kernel of coarse node = ptab[pidc(node)].
+ * Replaces ProlongationNet.forward + MultiGrid.Interpolate (FEANet/multigrid.py:62-73,124-130)
+ * and the `v + eF_delta` update (:179-180). */
+int fea_prolong_f32(const float* e, int C, float* out, const float* add, const uint8_t* pidc,
+                    const float* ptab, int ntab, float w1, int B, int Hc, int Wc, void* stream);
+int fea_prolong_f64(const double* e, int C, double* out, const double* add, const uint8_t* pidc,
+                    const double* ptab, int ntab, double w1, int B, int Hc, int Wc, void* stream);
+
+/* out[b] = || r[b, 0, 1:-1, 1:-1] ||_2 with r = f - K u (u may be the residual itself: pass
+ * f = NULL and ktab = NULL to take the norm of u).  Deterministic two-pass reduction; ws must
+ * hold fea_norm_workspace_bytes(B, max(H, W)) bytes.  Replaces the drivers'
+ * torch.norm(residual[:, :, 1:-1, 1:-1], dim=(2,3)) (M-FEANet-mg_test.ipynb:27428-27429). */
+int fea_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, const float* ktab, int ntab,
+                          double* out, double* ws, int B, int H, int W, void* stream);
+int fea_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
+                          double* out, double* ws, int B, int H, int W, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * (2) Framed multigrid-level ops (MultigridSolver), square N x N, N = 2^k + 1 >= 5.
+ *     `pid`/`pidc` are framed uint8 maps with the same ld (in bytes) as the T fields.
+ * ------------------------------------------------------------------------- */
+
+/* contiguous [B,1,N,N] -> framed, applying u*geo + bc (geo NULL: square, bc NULL: zero) */
+int fea_mg_pack_f32(const float* src, float* dst, const float* geo, long long geo_bstride,
+                    const float* bc, long long bc_bstride, int B, int N, int ld, long long bstride,
+                    void* stream);
+int fea_mg_pack_f64(const double* src, double* dst, const double* geo, long long geo_bstride,
+                    const double* bc, long long bc_bstride, int B, int N, int ld, long long bstride,
+                    void* stream);
+/* framed -> contiguous [B,1,N,N] */
+int fea_mg_unpack_f32(const float* src, float* dst, int B, int N, int ld, long long bstride, void* stream);
+int fea_mg_unpack_f64(const double* src, double* dst, int B, int N, int ld, long long bstride, void* stream);
+
+/* Interior sweep out = J(u, f) (boundary untouched).  u == NULL: zero initial guess
+ * (out = omd*f), the coarse-level pre-smooth of MultiGrid.iterate (FEANet/multigrid.py:171-172). */
+int fea_mg_sweep_f32(const float* u, const float* f, float* out, const uint8_t* pid, const float* ktab,
+                     const float* omd, int ntab, int B, int N, int ld, long long bstride, void* stream);
+int fea_mg_sweep_f64(const double* u, const double* f, double* out, const uint8_t* pid, const double* ktab,
+                     const double* omd, int ntab, int B, int N, int ld, long long bstride, void* stream);
+
+/* Fused residual + restriction: fc(interior) = w0 * R(f - K u), kernel by fine-node pattern.
+ * u == NULL: zero-initial-guess mode — the kernel first forms v = omd*f (the coarse-level
+ * pre-smooth), writes it to v_out, and restricts f - K v (one read of f for three ops:
+ * FEANet/multigrid.py:171-172 then :168-170).  (ldc, bstridec) = coarse layout. */
+int fea_mg_residual_restrict_f32(const float* u, const float* f, float* v_out, float* fc, const uint8_t* pid,
+                                 const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
+                                 float w0, int B, int N, int ld, long long bstride, int ldc,
+                                 long long bstridec, void* stream);
+int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out, double* fc,
+                                 const uint8_t* pid, const double* ktab, const double* omd, int ntab,
+                                 const double* rtab, int nrtab, double w0, int B, int N, int ld,
+                                 long long bstride, int ldc, long long bstridec, void* stream);
+
+/* Fused prolongation + correction + post-sweep:
+ *   out = J(u + w1 * P(ec), f)   (P kernel by coarse-node pattern pidc)
+ * FEANet/multigrid.py:177-181 (Interpolate, add, Relax) in one pass. */
+int fea_mg_prolong_sweep_f32(const float* u, const float* ec, const float* f, float* out, const uint8_t* pid,
+                             const uint8_t* pidc, const float* ktab, const float* omd, int ntab,
+                             const float* ptab, int nptab, float w1, int B, int N, int ld, long long bstride,
+                             int ldc, long long bstridec, void* stream);
+int fea_mg_prolong_sweep_f64(const double* u, const double* ec, const double* f, double* out,
+                             const uint8_t* pid, const uint8_t* pidc, const double* ktab, const double* omd,
+                             int ntab, const double* ptab, int nptab, double w1, int B, int N, int ld,
+                             long long bstride, int ldc, long long bstridec, void* stream);
+
+/* Prolongation + correction without a sweep (nu2 = 0 schedules): out = u + w1 * P(ec), interior. */
+int fea_mg_prolong_add_f32(const float* u, const float* ec, float* out, const uint8_t* pidc, const float* ptab,
+                           int nptab, float w1, int B, int N, int ld, long long bstride, int ldc,
+                           long long bstridec, void* stream);
+int fea_mg_prolong_add_f64(const double* u, const double* ec, double* out, const uint8_t* pidc,
+                           const double* ptab, int nptab, double w1, int B, int N, int ld, long long bstride,
+                           int ldc, long long bstridec, void* stream);
+
+/* out[b] = || (f - K u)[b, 1:-1, 1:-1] ||_2, deterministic; ws >= fea_norm_workspace_bytes(B, N). */
+int fea_mg_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, const float* ktab, int ntab,
+                             double* out, double* ws, int B, int N, int ld, long long bstride, void* stream);
+int fea_mg_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
+                             double* out, double* ws, int B, int N, int ld, long long bstride, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEANET_HIP_H */

@@ -1,0 +1,912 @@
+// framed_ops.hip — bandwidth-optimised multigrid level kernels on solver-owned FRAMED buffers.
+//
+// Layout (see include/feanet_hip.h): node (r, c) of sample b at
+//     base[b*bstride + (r+1)*ld + OFF + c],   OFF = A-1,  A = 128/sizeof(T)
+// so interior column 1 starts a 128-byte line and every 16-byte lane vector is aligned.
+//
+// Work decomposition ("column strip x row march", one wave = one independent task):
+//   * a wave owns a strip of SW = 64*VEC fine columns starting at c0 = 1 + s*SW (lane l holds
+//     columns c0 + VEC*l .. +VEC-1, VEC = 16/sizeof(T): one 16-byte load per lane per row, the
+//     whole row segment is one 1 KiB coalesced request);
+//   * it marches down RB rows keeping a 3-row window of the field in registers, so every input
+//     byte is read from HBM once (plus a 2-row / 2-line halo per task);
+//   * x-neighbours come from the adjacent lane via DPP wave_shr:1 / wave_shl:1; the two lanes at
+//     the strip edges take them from a 16-byte halo load (a line the neighbouring wave of the same
+//     block also reads, so it is an L1/L2 hit);
+//   * no LDS, no barriers in the stencil path (LDS only holds the <=16-pattern coefficient tables
+//     of the two-material problem), 4 independent waves per 256-thread block, XCD-aware block
+//     order so row-adjacent tasks share an L2.
+// Roofline: these kernels are HBM-bound (~0.9 flop/byte in fp64); algorithmic bytes per fine node
+// are documented in DESIGN.md (sweep 24 B, residual+restrict 18 B, prolong+sweep 26 B in fp64).
+#include "fea_common.h"
+
+namespace fea {
+
+template <typename T>
+struct Frame {
+  static constexpr int A = 128 / (int)sizeof(T);
+  static constexpr int OFF = A - 1;
+  static constexpr int VEC = 16 / (int)sizeof(T);
+  static constexpr int SW = kWave * VEC;
+};
+constexpr int kRB = 32;     // fine rows per task (even: tasks start on odd rows)
+constexpr int kWaves = 4;   // waves (tasks) per block
+constexpr int kTabStride = 10;  // LDS table row: 9 stencil weights + omega/d
+
+static inline int div_up(int a, int b) { return (a + b - 1) / b; }
+
+template <typename T>
+static inline int mg_nstrips(int N) { return div_up(N - 2, Frame<T>::SW); }
+
+template <typename T>
+static inline int mg_ld(int N) {
+  using F = Frame<T>;
+  const int need = F::OFF + 2 + std::max(mg_nstrips<T>(N) * F::SW + F::VEC, N + F::SW / 2 + 1);
+  return div_up(need, F::A) * F::A;
+}
+
+template <typename T>
+static inline long long mg_bstride(int N) { return (long long)(N + 2) * mg_ld<T>(N); }
+
+// ---------------------------------------------------------------------------
+// vector access helpers
+// ---------------------------------------------------------------------------
+template <typename T, int V>
+struct VecOf;
+template <>
+struct VecOf<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
+template <>
+struct VecOf<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
+template <>
+struct VecOf<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
+
+template <typename T, int V>
+__device__ __forceinline__ void vload(const T* p, T (&x)[V]) {
+  if constexpr (V == 1) {
+    x[0] = *p;
+  } else {
+    const typename VecOf<T, V>::type v = *reinterpret_cast<const typename VecOf<T, V>::type*>(p);
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] = v[k];
+  }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void vstore(T* p, const T (&x)[V]) {
+  if constexpr (V == 1) {
+    *p = x[0];
+  } else {
+    typename VecOf<T, V>::type v;
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = x[k];
+    *reinterpret_cast<typename VecOf<T, V>::type*>(p) = v;
+  }
+}
+
+// V pattern bytes -> ints
+template <int V>
+__device__ __forceinline__ void pload(const uint8_t* p, int (&o)[V]) {
+  if constexpr (V == 1) {
+    o[0] = p[0];
+  } else if constexpr (V == 2) {
+    const unsigned v = *reinterpret_cast<const unsigned short*>(p);
+    o[0] = v & 0xff;
+    o[1] = v >> 8;
+  } else {
+    const unsigned v = *reinterpret_cast<const unsigned*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (v >> (8 * k)) & 0xff;
+  }
+}
+
+// A row segment of one lane: a[0] = column c-1 (L), a[1..V] = own columns, a[V+1] = c+V (R),
+// a[V+2] = c+V+1 (RR).
+template <typename T, int V>
+struct Row {
+  T a[V + 3];
+};
+template <int V>
+struct PRow {  // LDS table offsets (pattern * kTabStride) for the same columns
+  int a[V + 3];
+};
+
+// Load one row segment (+ halos) of a framed field.  `rp` points at element (r, c0) of the strip.
+template <typename T, int V>
+__device__ __forceinline__ Row<T, V> load_row(const T* __restrict__ rp, int lane) {
+  Row<T, V> w;
+  T x[V], h[V];
+  vload<T, V>(rp + V * lane, x);
+  vload<T, V>(rp + (lane < 32 ? -V : kWave * V), h);  // lane 0: columns c0-V..c0-1; lane 63: c0+SW..
+#pragma unroll
+  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k];
+  w.a[0] = shr1(x[V - 1], h[V - 1]);
+  w.a[V + 1] = shl1(x[0], h[0]);
+  w.a[V + 2] = shl1(x[1 % V], h[1 % V]);
+  return w;
+}
+
+template <int V>
+__device__ __forceinline__ PRow<V> load_prow(const uint8_t* __restrict__ pp, int lane) {
+  PRow<V> w;
+  int x[V], h[V];
+  pload<V>(pp + V * lane, x);
+  pload<V>(pp + (lane < 32 ? -V : kWave * V), h);
+#pragma unroll
+  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * kTabStride;
+  w.a[0] = shr1(x[V - 1], h[V - 1]) * kTabStride;
+  w.a[V + 1] = shl1(x[0], h[0]) * kTabStride;
+  w.a[V + 2] = shl1(x[1 % V], h[1 % V]) * kTabStride;
+  return w;
+}
+
+// (K u) at own column k (k = 0..V, k = V is the R column) from the 3-row window.
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ T kapply(const Row<T, V>& w0, const Row<T, V>& w1, const Row<T, V>& w2,
+                                    const PRow<V>& p0, const PRow<V>& p1, const PRow<V>& p2, int k,
+                                    const T (&ks)[9], const T* tab) {
+  T acc;
+  if constexpr (!MULTI) {
+    acc = ks[0] * w0.a[k];
+    acc += ks[1] * w0.a[k + 1];
+    acc += ks[2] * w0.a[k + 2];
+    acc += ks[3] * w1.a[k];
+    acc += ks[4] * w1.a[k + 1];
+    acc += ks[5] * w1.a[k + 2];
+    acc += ks[6] * w2.a[k];
+    acc += ks[7] * w2.a[k + 1];
+    acc += ks[8] * w2.a[k + 2];
+  } else {
+    acc = tab[p0.a[k] + 0] * w0.a[k];
+    acc += tab[p0.a[k + 1] + 1] * w0.a[k + 1];
+    acc += tab[p0.a[k + 2] + 2] * w0.a[k + 2];
+    acc += tab[p1.a[k] + 3] * w1.a[k];
+    acc += tab[p1.a[k + 1] + 4] * w1.a[k + 1];
+    acc += tab[p1.a[k + 2] + 5] * w1.a[k + 2];
+    acc += tab[p2.a[k] + 6] * w2.a[k];
+    acc += tab[p2.a[k + 1] + 7] * w2.a[k + 1];
+    acc += tab[p2.a[k + 2] + 8] * w2.a[k + 2];
+  }
+  return acc;
+}
+
+template <typename T>
+struct MgArgs {
+  const T* u;
+  const T* f;
+  T* out;
+  T* out2;
+  const T* ec;
+  const uint8_t* pid;
+  const uint8_t* pidc;
+  const T* ktab;
+  const T* omd;
+  const T* rtab;
+  const T* ptab;
+  double* part;
+  int ntab, nrtab, nptab;
+  T w;
+  int N, ld;
+  long long bs;
+  int Nc, ldc;
+  long long bsc;
+  int nstrips, ntr;  // strips per row, row tasks per sample
+};
+
+struct TaskId {
+  int b, s, t;
+  bool valid;
+};
+
+__device__ __forceinline__ TaskId decode_task(int nstrips, int ntr) {
+  const int nsg = (nstrips + kWaves - 1) / kWaves;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_b = ntr * nsg;
+  TaskId id;
+  id.b = bid / per_b;
+  const int rem = bid - id.b * per_b;
+  id.t = rem / nsg;
+  const int sg = rem - id.t * nsg;
+  id.s = sg * kWaves + (threadIdx.x >> 6);
+  id.valid = id.s < nstrips;
+  return id;
+}
+
+// Loads ktab/omd (stride 10) and optionally a second 9-wide table into LDS.
+template <typename T>
+__device__ __forceinline__ void load_tables(T* tab, const T* ktab, const T* omd, int ntab, T* tab2,
+                                            const T* t2, int n2) {
+  for (int i = threadIdx.x; i < ntab * kTabStride; i += blockDim.x) {
+    const int p = i / kTabStride, d = i - p * kTabStride;
+    tab[i] = (d == 9) ? (omd ? omd[p] : T(0)) : ktab[p * 9 + d];
+  }
+  if (tab2)
+    for (int i = threadIdx.x; i < n2 * kTabStride; i += blockDim.x) {
+      const int p = i / kTabStride, d = i - p * kTabStride;
+      tab2[i] = (d == 9) ? T(0) : t2[p * 9 + d];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel A: interior Jacobi sweep  out = J(u, f);  ZERO: u == 0  ->  out = omd * f
+// ---------------------------------------------------------------------------
+template <typename T, bool MULTI, bool ZERO>
+__global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
+  using F = Frame<T>;
+  constexpr int V = F::VEC;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, nullptr, nullptr, 0);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int N = g.N;
+  const int c0 = 1 + id.s * F::SW;
+  const int r0 = 1 + id.t * kRB;
+  const int r1 = min(r0 + kRB, N - 1);
+  const int cl = c0 + V * lane;  // first own column
+  const bool full = cl + V - 1 <= N - 2;
+  T ks[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) ks[d] = g.ktab[d];
+    om = g.omd[0];
+  }
+  const long long poff = F::OFF + c0;
+  const long long boff = (long long)id.b * g.bs + poff;
+  const T* __restrict__ ub = g.u + boff;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ ob = g.out + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;  // pattern maps: one per mesh
+  const int ld = g.ld;
+
+  if constexpr (ZERO) {
+    for (int r = r0; r < r1; ++r) {
+      const long long ro = (long long)(r + 1) * ld + V * lane;
+      T fv[V], o[V];
+      vload<T, V>(fb + ro, fv);
+      int pv[V];
+      if constexpr (MULTI) pload<V>(pb + ro, pv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = (MULTI ? tab[pv[k] * kTabStride + 9] : om) * fv[k];
+      if (full) {
+        vstore<T, V>(ob + ro, o);
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (cl + k <= N - 2) ob[ro + k] = o[k];
+      }
+    }
+    return;
+  } else {
+    Row<T, V> w0 = load_row<T, V>(ub + (long long)r0 * ld, lane);
+    Row<T, V> w1 = load_row<T, V>(ub + (long long)(r0 + 1) * ld, lane);
+    PRow<V> p0{}, p1{}, p2{};
+    if constexpr (MULTI) {
+      p0 = load_prow<V>(pb + (long long)r0 * ld, lane);
+      p1 = load_prow<V>(pb + (long long)(r0 + 1) * ld, lane);
+    }
+    for (int r = r0; r < r1; ++r) {
+      const long long ro = (long long)(r + 1) * ld;
+      const Row<T, V> w2 = load_row<T, V>(ub + ro + ld, lane);
+      if constexpr (MULTI) p2 = load_prow<V>(pb + ro + ld, lane);
+      T fv[V], o[V];
+      vload<T, V>(fb + ro + V * lane, fv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const T acc = kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
+        const T omk = MULTI ? tab[p1.a[k + 1] + 9] : om;
+        o[k] = omk * (fv[k] - acc) + w1.a[k + 1];
+      }
+      if (full) {
+        vstore<T, V>(ob + ro + V * lane, o);
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (cl + k <= N - 2) ob[ro + V * lane + k] = o[k];
+      }
+      w0 = w1;
+      w1 = w2;
+      if constexpr (MULTI) {
+        p0 = p1;
+        p1 = p2;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel B: fused residual + restriction (+ optional zero-guess pre-sweep).
+//   task = (strip s, coarse rows [I0, I1)), fine rows 2I0-2 .. 2I1 are read.
+// ---------------------------------------------------------------------------
+template <typename T, bool MULTI, bool ZERO>
+__global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
+  using F = Frame<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;  // coarse outputs per lane
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int N = g.N, Nc = g.Nc;
+  const int c0 = 1 + id.s * F::SW;
+  const int I0 = 1 + id.t * (kRB / 2);
+  const int I1 = min(I0 + kRB / 2, Nc - 1);
+  const int cl = c0 + V * lane;
+  T ks[9], rs[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      rs[d] = g.rtab[d];
+    }
+    om = g.omd ? g.omd[0] : T(0);
+  }
+  const T w0 = g.w;
+  // interior mask of the lane's V+3 window columns (ZERO mode derives v = omd*f inside only)
+  bool cin[V + 3];
+#pragma unroll
+  for (int j = 0; j < V + 3; ++j) {
+    const int c = cl + j - 1;
+    cin[j] = c >= 1 && c <= N - 2;
+  }
+  const long long poff = F::OFF + c0;
+  const long long boff = (long long)id.b * g.bs + poff;
+  const T* __restrict__ ub = ZERO ? nullptr : g.u + boff;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ vb = ZERO ? g.out2 + boff : nullptr;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
+  const int ld = g.ld;
+  const int bc0 = (c0 + 1) / 2;  // coarse column of lane 0's first output
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
+  const int Jl = bc0 + Q * lane;
+
+  // one "window row": the field used by K (u, or v = omd*f in ZERO mode), plus the raw f row
+  // (ZERO mode: the same load) and pattern offsets.
+  struct WRow {
+    Row<T, V> u;
+    Row<T, V> f;
+    PRow<V> p;
+  };
+  auto load_w = [&](int y) {
+    WRow w;
+    const long long ro = (long long)(y + 1) * ld;
+    if constexpr (MULTI) w.p = load_prow<V>(pb + ro, lane);
+    w.f = load_row<T, V>(fb + ro, lane);
+    if constexpr (ZERO) {
+      const bool rin = y >= 1 && y <= N - 2;
+#pragma unroll
+      for (int j = 0; j < V + 3; ++j) {
+        const T omj = MULTI ? tab[w.p.a[j] + 9] : om;
+        w.u.a[j] = (rin && cin[j]) ? omj * w.f.a[j] : T(0);
+      }
+    } else {
+      w.u = load_row<T, V>(ub + ro, lane);
+    }
+    return w;
+  };
+  // residual at own columns k = 0..V of the centre row (f at those columns from the f row)
+  auto resid = [&](const WRow& a, const WRow& b, const WRow& c, T (&r)[V + 1]) {
+#pragma unroll
+    for (int k = 0; k <= V; ++k) r[k] = b.f.a[k + 1] - kapply<T, V, MULTI>(a.u, b.u, c.u, a.p, b.p, c.p, k, ks, tab);
+  };
+  auto store_v = [&](int y, const WRow& w) {
+    if constexpr (ZERO) {
+      const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Nc - 1) && y <= N - 2;
+      if (own) {
+        T* vp = vb + (long long)(y + 1) * ld + V * lane;
+        if (cl + V - 1 <= N - 2) {
+          T o[V];
+#pragma unroll
+          for (int k = 0; k < V; ++k) o[k] = w.u.a[k + 1];
+          vstore<T, V>(vp, o);
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k)
+            if (cl + k <= N - 2) vp[k] = w.u.a[k + 1];
+        }
+      }
+    }
+  };
+
+  const int y0 = 2 * I0 - 1;
+  WRow W0 = load_w(y0 - 1);
+  WRow W1 = load_w(y0);
+  WRow W2 = load_w(y0 + 1);
+  T Ra[V + 1], Rb[V + 1], Rc[V + 1];
+  PRow<V> Pa = W1.p, Pb, Pc;
+  resid(W0, W1, W2, Ra);
+  store_v(y0, W1);
+  for (int I = I0; I < I1; ++I) {
+    // fine row 2I
+    W0 = W1;
+    W1 = W2;
+    W2 = load_w(2 * I + 1);
+    resid(W0, W1, W2, Rb);
+    Pb = W1.p;
+    store_v(2 * I, W1);
+    // fine row 2I+1
+    W0 = W1;
+    W1 = W2;
+    W2 = load_w(2 * I + 2);
+    resid(W0, W1, W2, Rc);
+    Pc = W1.p;
+    store_v(2 * I + 1, W1);
+    // coarse row I: outputs q use fine columns 2q, 2q+1, 2q+2 of the residual rows
+    T o[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      T acc;
+      if constexpr (!MULTI) {
+        acc = rs[0] * Ra[2 * q];
+        acc += rs[1] * Ra[2 * q + 1];
+        acc += rs[2] * Ra[2 * q + 2];
+        acc += rs[3] * Rb[2 * q];
+        acc += rs[4] * Rb[2 * q + 1];
+        acc += rs[5] * Rb[2 * q + 2];
+        acc += rs[6] * Rc[2 * q];
+        acc += rs[7] * Rc[2 * q + 1];
+        acc += rs[8] * Rc[2 * q + 2];
+      } else {
+        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
+        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
+        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
+        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
+        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
+        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
+        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
+        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
+        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+      }
+      o[q] = w0 * acc;
+    }
+    T* cp = cb + (long long)(I + 1) * g.ldc;
+    if (Jl + Q - 1 <= Nc - 2) {
+      vstore<T, Q>(cp, o);
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (Jl + q <= Nc - 2) cp[q] = o[q];
+    }
+#pragma unroll
+    for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
+    Pa = Pc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel C: fused prolongation + correction (+ post-sweep):
+//   v = u + w1 * P(ec)   (P kernel of the coarse node);   out = SWEEP ? J(v, f) : v
+// ---------------------------------------------------------------------------
+template <typename T, int V>
+struct CRow {  // coarse row at coarse columns b_base-1 .. b_base+V/2 (V/2+2 values)
+  T e[V / 2 + 2];
+  int o[V / 2 + 2];
+};
+
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ CRow<T, V> load_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp,
+                                                int lane) {
+  constexpr int Q = V / 2;
+  CRow<T, V> c;
+  T x[Q];
+  vload<T, Q>(ep + Q * lane, x);
+  const T h = ep[lane < 32 ? -1 : kWave * Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) c.e[q + 1] = x[q];
+  c.e[0] = shr1(x[Q - 1], h);
+  c.e[Q + 1] = shl1(x[0], h);
+  if constexpr (MULTI) {
+    int px[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) px[q] = pp[Q * lane + q];
+    const int ph = pp[lane < 32 ? -1 : kWave * Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c.o[q + 1] = px[q] * kTabStride;
+    c.o[0] = shr1(px[Q - 1], ph) * kTabStride;
+    c.o[Q + 1] = shl1(px[0], ph) * kTabStride;
+  }
+  return c;
+}
+
+// coarse row contribution sum_b P[pc(a,b)][ky][kx] e(a,b) at window column j (k = j-1)
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ T crow_term(const CRow<T, V>& c, int j, int ky, const T (&ps)[9], const T* ptb) {
+  const int k = j - 1;
+  if ((k & 1) != 0) {  // even fine column: one coarse node, kx = 1
+    const int i = (k + 1) / 2;
+    return (MULTI ? ptb[c.o[i] + ky * 3 + 1] : ps[ky * 3 + 1]) * c.e[i];
+  } else {  // odd fine column: coarse nodes k/2 (kx = 2) and k/2+1 (kx = 0)
+    const int i = k / 2;
+    T t = (MULTI ? ptb[c.o[i] + ky * 3 + 2] : ps[ky * 3 + 2]) * c.e[i];
+    t += (MULTI ? ptb[c.o[i + 1] + ky * 3 + 0] : ps[ky * 3 + 0]) * c.e[i + 1];
+    return t;
+  }
+}
+
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ void correct_even(Row<T, V>& u, const CRow<T, V>& ca, T w1, const T (&ps)[9],
+                                             const T* ptb) {
+#pragma unroll
+  for (int j = 0; j <= V + 1; ++j) u.a[j] += w1 * crow_term<T, V, MULTI>(ca, j, 1, ps, ptb);
+}
+
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ void correct_odd(Row<T, V>& u, const CRow<T, V>& ca, const CRow<T, V>& cb, T w1,
+                                            const T (&ps)[9], const T* ptb) {
+#pragma unroll
+  for (int j = 0; j <= V + 1; ++j) {
+    const T t = crow_term<T, V, MULTI>(ca, j, 2, ps, ptb) + crow_term<T, V, MULTI>(cb, j, 0, ps, ptb);
+    u.a[j] += w1 * t;
+  }
+}
+
+template <typename T, bool MULTI, bool SWEEP>
+__global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
+  using F = Frame<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, SWEEP ? g.ktab : g.ptab, SWEEP ? g.omd : nullptr, SWEEP ? g.ntab : 0, ptb, g.ptab,
+                   g.nptab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int N = g.N;
+  const int c0 = 1 + id.s * F::SW;
+  const int r0 = 1 + id.t * kRB;  // odd
+  const int r1 = min(r0 + kRB, N - 1);
+  const int cl = c0 + V * lane;
+  const bool full = cl + V - 1 <= N - 2;
+  T ks[9], ps[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = SWEEP ? g.ktab[d] : T(0);
+      ps[d] = g.ptab[d];
+    }
+    om = SWEEP ? g.omd[0] : T(0);
+  }
+  const T w1 = g.w;
+  const int ld = g.ld, ldc = g.ldc;
+  const long long poff = F::OFF + c0;
+  const long long boff = (long long)id.b * g.bs + poff;
+  const T* __restrict__ ub = g.u + boff;
+  const T* __restrict__ fb = SWEEP ? g.f + boff : nullptr;
+  T* __restrict__ ob = g.out + boff;
+  const uint8_t* __restrict__ pb = (MULTI && SWEEP) ? g.pid + poff : nullptr;
+  const int bc0 = (c0 + 1) / 2;
+  const long long pcoff = F::OFF + bc0;
+  const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + pcoff;
+  const uint8_t* __restrict__ pcb = MULTI ? g.pidc + pcoff : nullptr;
+
+  auto crow = [&](int a) { return load_crow<T, V, MULTI>(eb + (long long)(a + 1) * ldc, MULTI ? pcb + (long long)(a + 1) * ldc : nullptr, lane); };
+  auto urow = [&](int y) { return load_row<T, V>(ub + (long long)(y + 1) * ld, lane); };
+  auto prow = [&](int y) {
+    PRow<V> p{};
+    if constexpr (MULTI && SWEEP) p = load_prow<V>(pb + (long long)(y + 1) * ld, lane);
+    return p;
+  };
+  auto emit = [&](int y, const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
+                  const PRow<V>& pbb, const PRow<V>& pc) {
+    const long long ro = (long long)(y + 1) * ld + V * lane;
+    T o[V];
+    if constexpr (SWEEP) {
+      T fv[V];
+      vload<T, V>(fb + ro, fv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const T acc = kapply<T, V, MULTI>(a, b, c, pa, pbb, pc, k, ks, tab);
+        const T omk = MULTI ? tab[pbb.a[k + 1] + 9] : om;
+        o[k] = omk * (fv[k] - acc) + b.a[k + 1];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = b.a[k + 1];
+    }
+    if (full) {
+      vstore<T, V>(ob + ro, o);
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        if (cl + k <= N - 2) ob[ro + k] = o[k];
+    }
+  };
+
+  // window rows r0-1 (even, coarse a0) and r0 (odd, coarse a0, a0+1)
+  const int a0 = (r0 - 1) / 2;
+  CRow<T, V> C0 = crow(a0), C1 = crow(a0 + 1);
+  Row<T, V> Vp = urow(r0 - 1), Vc = urow(r0);
+  correct_even<T, V, MULTI>(Vp, C0, w1, ps, ptb);
+  correct_odd<T, V, MULTI>(Vc, C0, C1, w1, ps, ptb);
+  PRow<V> Pp = prow(r0 - 1), Pc = prow(r0);
+  for (int y = r0; y < r1; y += 2) {
+    // row y+1 (even, coarse (y+1)/2 = C1)
+    Row<T, V> Vn = urow(y + 1);
+    correct_even<T, V, MULTI>(Vn, C1, w1, ps, ptb);
+    PRow<V> Pn = prow(y + 1);
+    emit(y, Vp, Vc, Vn, Pp, Pc, Pn);
+    if (y + 1 < r1) {
+      // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
+      const CRow<T, V> C2 = crow((y + 3) / 2);
+      Row<T, V> Vnn = urow(y + 2);
+      correct_odd<T, V, MULTI>(Vnn, C1, C2, w1, ps, ptb);
+      PRow<V> Pnn = prow(y + 2);
+      emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn);
+      Vp = Vn;
+      Vc = Vnn;
+      Pp = Pn;
+      Pc = Pnn;
+      C1 = C2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel D: per-task partial sums of (f - K u)^2 over the interior (deterministic).
+// ---------------------------------------------------------------------------
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
+  using F = Frame<T>;
+  constexpr int V = F::VEC;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, nullptr, g.ntab, nullptr, nullptr, 0);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int N = g.N;
+  const int c0 = 1 + id.s * F::SW;
+  const int r0 = 1 + id.t * kRB;
+  const int r1 = min(r0 + kRB, N - 1);
+  const int cl = c0 + V * lane;
+  T ks[9];
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) ks[d] = g.ktab[d];
+  }
+  const long long poff = F::OFF + c0;
+  const long long boff = (long long)id.b * g.bs + poff;
+  const T* __restrict__ ub = g.u + boff;
+  const T* __restrict__ fb = g.f + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
+  const int ld = g.ld;
+  Row<T, V> w0 = load_row<T, V>(ub + (long long)r0 * ld, lane);
+  Row<T, V> w1 = load_row<T, V>(ub + (long long)(r0 + 1) * ld, lane);
+  PRow<V> p0{}, p1{}, p2{};
+  if constexpr (MULTI) {
+    p0 = load_prow<V>(pb + (long long)r0 * ld, lane);
+    p1 = load_prow<V>(pb + (long long)(r0 + 1) * ld, lane);
+  }
+  double s = 0.0;
+  for (int r = r0; r < r1; ++r) {
+    const long long ro = (long long)(r + 1) * ld;
+    const Row<T, V> w2 = load_row<T, V>(ub + ro + ld, lane);
+    if constexpr (MULTI) p2 = load_prow<V>(pb + ro + ld, lane);
+    T fv[V];
+    vload<T, V>(fb + ro + V * lane, fv);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T rr = fv[k] - kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
+      if (cl + k <= N - 2) s += (double)rr * (double)rr;
+    }
+    w0 = w1;
+    w1 = w2;
+    if constexpr (MULTI) {
+      p0 = p1;
+      p1 = p2;
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) g.part[(long long)id.b * g.ntr * g.nstrips + (long long)id.t * g.nstrips + id.s] = s;
+}
+
+// ---------------------------------------------------------------------------
+// pack / unpack between contiguous [B,1,N,N] and the framed layout
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_mg_pack(const T* __restrict__ src, T* __restrict__ dst,
+                                                 const T* __restrict__ geo, long long geo_bs,
+                                                 const T* __restrict__ bc, long long bc_bs, int N, int ld,
+                                                 long long bs) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), r = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
+  if (r >= N || c >= N) return;
+  const long long i = (long long)r * N + c;
+  const T v = src[(long long)b * N * N + i];
+  const T gv = geo ? geo[b * geo_bs + i] : T((r > 0 && r < N - 1 && c > 0 && c < N - 1) ? 1 : 0);
+  const T bv = bc ? bc[b * bc_bs + i] : T(0);
+  dst[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c] = v * gv + bv;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_mg_unpack(const T* __restrict__ src, T* __restrict__ dst, int N, int ld,
+                                                   long long bs) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), r = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
+  if (r >= N || c >= N) return;
+  dst[(long long)b * N * N + (long long)r * N + c] = src[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c];
+}
+
+}  // namespace fea
+
+using namespace fea;
+
+static inline bool mg_n_ok(int N) {
+  if (N < 3 || N > (1 << 20) + 1) return false;
+  const int n = N - 1;
+  return (n & (n - 1)) == 0;
+}
+
+template <typename T>
+static MgArgs<T> mg_args(int N, int ld, long long bs) {
+  MgArgs<T> g{};
+  g.N = N;
+  g.ld = ld;
+  g.bs = bs;
+  g.nstrips = mg_nstrips<T>(N);
+  g.ntr = div_up(N - 2, kRB);
+  return g;
+}
+
+template <typename T>
+static inline bool layout_ok(int N, int ld, long long bs) {
+  return mg_n_ok(N) && ld >= mg_ld<T>(N) && ld % Frame<T>::A == 0 && bs >= (long long)(N + 2) * ld;
+}
+
+static inline dim3 mg_grid(int B, int ntr, int nstrips) {
+  return dim3((unsigned)(B * ntr * div_up(nstrips, kWaves)));
+}
+
+extern "C" int fea_abi_version(void) { return 1; }
+
+extern "C" int fea_mg_layout(int N, int elem_size, int* ld, long long* bstride) {
+  if (!mg_n_ok(N) || !ld || !bstride) return FEA_EINVAL;
+  if (elem_size == 8) {
+    *ld = mg_ld<double>(N);
+    *bstride = mg_bstride<double>(N);
+  } else if (elem_size == 4) {
+    *ld = mg_ld<float>(N);
+    *bstride = mg_bstride<float>(N);
+  } else {
+    return FEA_EINVAL;
+  }
+  return 0;
+}
+
+extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
+  if (B <= 0 || N <= 0) return 0;
+  // generic: one partial per 64x4 block; framed: one per (strip, row task) at the fp32 strip width
+  const long long gen = (long long)div_up(N, 64) * div_up(N, 4);
+  const long long frm = (long long)div_up(N, 64) * div_up(N, kRB);
+  return (size_t)B * (size_t)std::max(gen, frm) * sizeof(double);
+}
+
+#define FEA_MG_API(SUF, T)                                                                                   \
+  extern "C" int fea_mg_pack_##SUF(const T* src, T* dst, const T* geo, long long geo_bs, const T* bc,         \
+                                   long long bc_bs, int B, int N, int ld, long long bs, void* stream) {       \
+    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                   \
+    k_mg_pack<T><<<dim3(div_up(N, 64), div_up(N, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, geo, geo_bs, \
+                                                                                       bc, bc_bs, N, ld, bs); \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_mg_unpack_##SUF(const T* src, T* dst, int B, int N, int ld, long long bs, void* stream) { \
+    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                   \
+    k_mg_unpack<T><<<dim3(div_up(N, 64), div_up(N, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, N, ld,  \
+                                                                                         bs);                \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_mg_sweep_##SUF(const T* u, const T* f, T* out, const uint8_t* pid, const T* ktab,         \
+                                    const T* omd, int ntab, int B, int N, int ld, long long bs, void* stream) { \
+    if (!f || !out || !ktab || !omd || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                 \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || out == u) return FEA_EINVAL;             \
+    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    g.u = u; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;                   \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    const bool multi = ntab > 1;                                                                             \
+    if (!u) {                                                                                                \
+      if (multi) k_mg_sweep<T, true, true><<<grid, 256, 0, s>>>(g);                                          \
+      else k_mg_sweep<T, false, true><<<grid, 256, 0, s>>>(g);                                               \
+    } else {                                                                                                 \
+      if (multi) k_mg_sweep<T, true, false><<<grid, 256, 0, s>>>(g);                                         \
+      else k_mg_sweep<T, false, false><<<grid, 256, 0, s>>>(g);                                              \
+    }                                                                                                        \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_mg_residual_restrict_##SUF(const T* u, const T* f, T* v_out, T* fc, const uint8_t* pid, \
+                                                const T* ktab, const T* omd, int ntab, const T* rtab,          \
+                                                int nrtab, T w0, int B, int N, int ld, long long bs, int ldc,  \
+                                                long long bsc, void* stream) {                               \
+    if (!f || !fc || !ktab || !rtab || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                  \
+    const int Nc = (N + 1) / 2;                                                                              \
+    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
+    if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;                                                      \
+    if (!u && (!v_out || !omd)) return FEA_EINVAL;                                                           \
+    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    g.u = u; g.f = f; g.out = fc; g.out2 = v_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
+    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;                           \
+    g.ntr = div_up(Nc - 2, kRB / 2);                                                                         \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    const bool multi = ntab > 1;                                                                             \
+    if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
+    if (!u) {                                                                                                \
+      if (multi) k_mg_resid_restrict<T, true, true><<<grid, 256, 0, s>>>(g);                                 \
+      else k_mg_resid_restrict<T, false, true><<<grid, 256, 0, s>>>(g);                                      \
+    } else {                                                                                                 \
+      if (multi) k_mg_resid_restrict<T, true, false><<<grid, 256, 0, s>>>(g);                                \
+      else k_mg_resid_restrict<T, false, false><<<grid, 256, 0, s>>>(g);                                     \
+    }                                                                                                        \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \
+                              const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab,      \
+                              int nptab, T w1, int B, int N, int ld, long long bs, int ldc, long long bsc,   \
+                              void* stream, bool sweep) {                                                    \
+    if (!u || !ec || !out || !ptab || B <= 0 || !layout_ok<T>(N, ld, bs) || out == u) return FEA_EINVAL;      \
+    const int Nc = (N + 1) / 2;                                                                              \
+    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+    if (nptab < 1 || nptab > FEA_MAX_PATTERNS || (nptab > 1 && !pidc)) return FEA_EINVAL;                    \
+    if (sweep && (!f || !ktab || !omd || ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)))          \
+      return FEA_EINVAL;                                                                                     \
+    const bool multi = nptab > 1 || (sweep && ntab > 1);                                                     \
+    if (multi && ((sweep && (!pid || ntab == 1)) || !pidc || nptab == 1)) return FEA_EINVAL;                 \
+    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    g.u = u; g.ec = ec; g.f = f; g.out = out; g.pid = pid; g.pidc = pidc; g.ktab = ktab; g.omd = omd;         \
+    g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;            \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (sweep) {                                                                                             \
+      if (multi) k_mg_prolong<T, true, true><<<grid, 256, 0, s>>>(g);                                        \
+      else k_mg_prolong<T, false, true><<<grid, 256, 0, s>>>(g);                                             \
+    } else {                                                                                                 \
+      if (multi) k_mg_prolong<T, true, false><<<grid, 256, 0, s>>>(g);                                       \
+      else k_mg_prolong<T, false, false><<<grid, 256, 0, s>>>(g);                                            \
+    }                                                                                                        \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_mg_prolong_sweep_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,  \
+                                            const uint8_t* pidc, const T* ktab, const T* omd, int ntab,       \
+                                            const T* ptab, int nptab, T w1, int B, int N, int ld,            \
+                                            long long bs, int ldc, long long bsc, void* stream) {             \
+    return mg_prolong_##SUF(u, ec, f, out, pid, pidc, ktab, omd, ntab, ptab, nptab, w1, B, N, ld, bs, ldc,   \
+                            bsc, stream, true);                                                              \
+  }                                                                                                          \
+  extern "C" int fea_mg_prolong_add_##SUF(const T* u, const T* ec, T* out, const uint8_t* pidc, const T* ptab, \
+                                          int nptab, T w1, int B, int N, int ld, long long bs, int ldc,       \
+                                          long long bsc, void* stream) {                                     \
+    return mg_prolong_##SUF(u, ec, nullptr, out, nullptr, pidc, nullptr, nullptr, 0, ptab, nptab, w1, B, N,  \
+                            ld, bs, ldc, bsc, stream, false);                                                \
+  }                                                                                                          \
+  extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \
+                                            int ntab, double* out, double* ws, int B, int N, int ld,          \
+                                            long long bs, void* stream) {                                    \
+    if (!u || !f || !ktab || !out || !ws || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;            \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
+    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    g.u = u; g.f = f; g.pid = pid; g.ktab = ktab; g.ntab = ntab; g.part = ws;                                \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (ntab > 1) k_mg_resnorm<T, true><<<grid, 256, 0, s>>>(g);                                             \
+    else k_mg_resnorm<T, false><<<grid, 256, 0, s>>>(g);                                                     \
+    k_norm_final<<<B, 256, 0, s>>>(ws, (long long)g.ntr * g.nstrips, out);                               \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }
+
+FEA_MG_API(f32, float)
+FEA_MG_API(f64, double)

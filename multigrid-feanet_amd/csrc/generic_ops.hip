@@ -1,0 +1,322 @@
+// generic_ops.hip — FEANet operators on contiguous NCHW tensors (the drop-in operator
+// boundary behind FEANet.model / FEANet.jacobi / FEANet.multigrid shims).
+//
+// These kernels take arbitrary contiguous user tensors (row pitch = W, any alignment), so they
+// are written one-output-per-lane with the 3x3 neighbourhood read through L1/L2; the
+// bandwidth-optimised path for the V-cycle is framed_ops.hip (solver-owned aligned buffers).
+#include "fea_common.h"
+
+namespace fea {
+
+constexpr int kBX = 64, kBY = 4;  // one wave per block row
+
+template <typename T>
+__device__ __forceinline__ void load_table(T* dst, const T* src, int n) {
+  for (int i = threadIdx.y * blockDim.x + threadIdx.x; i < n; i += blockDim.x * blockDim.y) dst[i] = src[i];
+}
+
+// y = K u  (FEANet/model.py:22-30): weight of neighbour j is ktab[pid(j)][d], zero padding.
+template <typename T>
+__global__ __launch_bounds__(256) void k_knet(const T* __restrict__ u, T* __restrict__ y,
+                                              const uint8_t* __restrict__ pid, const T* __restrict__ ktab,
+                                              int ntab, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, ktab, ntab * 9);
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W;
+  const T* ub = u + blockIdx.z * HW;
+  T acc = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const int rr = r + dr - 1;
+    if (rr < 0 || rr >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int cc = c + dc - 1;
+      if (cc < 0 || cc >= W) continue;
+      const int p = pid ? pid[rr * W + cc] : 0;
+      acc += tab[p * 9 + dr * 3 + dc] * ub[(long long)rr * W + cc];
+    }
+  }
+  y[blockIdx.z * HW + (long long)r * W + c] = acc;
+}
+
+// xs[b, p] = (pid == p) ? x[b] : 0  (FEANet/model.py:37-47)
+template <typename T>
+__global__ __launch_bounds__(256) void k_split(const T* __restrict__ x, T* __restrict__ xs,
+                                               const uint8_t* __restrict__ pid, int C, int H, int W) {
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W, i = (long long)r * W + c;
+  const T v = x[blockIdx.z * HW + i];
+  const int p = pid ? pid[i] : 0;
+  T* o = xs + (long long)blockIdx.z * C * HW + i;
+  for (int ch = 0; ch < C; ++ch) o[ch * HW] = (ch == p) ? v : T(0);
+}
+
+template <typename T>
+__device__ __forceinline__ T reset_at(const T* geo, const T* bc, long long gi, long long bi, T v, int r, int c,
+                                      int H, int W) {
+  const T g = geo ? geo[gi] : T((r > 0 && r < H - 1 && c > 0 && c < W - 1) ? 1 : 0);
+  const T b = bc ? bc[bi] : T(0);
+  return v * g + b;
+}
+
+// One weighted-Jacobi sweep (FEANet/jacobi.py:39-47) with reset_boundary (:27-29) on both sides.
+template <typename T>
+__global__ __launch_bounds__(256) void k_jacobi(const T* __restrict__ u, const T* __restrict__ f,
+                                                T* __restrict__ out, const uint8_t* __restrict__ pid,
+                                                const T* __restrict__ ktab, const T* __restrict__ omd, int ntab,
+                                                const T* __restrict__ geo, long long geo_bs,
+                                                const T* __restrict__ bc, long long bc_bs, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 10];
+  for (int i = threadIdx.y * blockDim.x + threadIdx.x; i < ntab * 10; i += blockDim.x * blockDim.y)
+    tab[i] = (i % 10 == 9) ? omd[i / 10] : ktab[(i / 10) * 9 + (i % 10)];
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W;
+  const int b = blockIdx.z;
+  const T* ub = u + b * HW;
+  const T* gb = geo ? geo + b * geo_bs : nullptr;
+  const T* bb = bc ? bc + b * bc_bs : nullptr;
+  T acc = 0, u0c = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const int rr = r + dr - 1;
+    if (rr < 0 || rr >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int cc = c + dc - 1;
+      if (cc < 0 || cc >= W) continue;
+      const long long j = (long long)rr * W + cc;
+      const T v0 = reset_at(gb, bb, j, j, ub[j], rr, cc, H, W);
+      if (dr == 1 && dc == 1) u0c = v0;
+      const int p = pid ? pid[j] : 0;
+      acc += tab[p * 10 + dr * 3 + dc] * v0;
+    }
+  }
+  const long long i = (long long)r * W + c;
+  const int p = pid ? pid[i] : 0;
+  const T res = f[b * HW + i] - acc;
+  const T u1 = tab[p * 10 + 9] * res + u0c;
+  out[b * HW + i] = reset_at(gb, bb, i, i, u1, r, c, H, W);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_residual(const T* __restrict__ u, const T* __restrict__ f,
+                                                  T* __restrict__ res, const uint8_t* __restrict__ pid,
+                                                  const T* __restrict__ ktab, int ntab, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, ktab, ntab * 9);
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W;
+  const T* ub = u + blockIdx.z * HW;
+  T acc = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const int rr = r + dr - 1;
+    if (rr < 0 || rr >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int cc = c + dc - 1;
+      if (cc < 0 || cc >= W) continue;
+      const int p = pid ? pid[rr * W + cc] : 0;
+      acc += tab[p * 9 + dr * 3 + dc] * ub[(long long)rr * W + cc];
+    }
+  }
+  const long long i = blockIdx.z * HW + (long long)r * W + c;
+  res[i] = f[i] - acc;
+}
+
+// fc = w0 * pad0(conv2d(x[..,1:-1,1:-1], R, stride 2)); C>1: split input, channel kernels.
+template <typename T>
+__global__ __launch_bounds__(256) void k_restrict(const T* __restrict__ x, int C, T* __restrict__ fc,
+                                                  const uint8_t* __restrict__ pid, const T* __restrict__ rtab,
+                                                  int ntab, T w0, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, rtab, ntab * 9);
+  __syncthreads();
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int J = blockIdx.x * kBX + threadIdx.x, I = blockIdx.y * kBY + threadIdx.y;
+  if (I >= Hc || J >= Wc) return;
+  const long long HW = (long long)H * W;
+  T acc = 0;
+  if (I > 0 && I < Hc - 1 && J > 0 && J < Wc - 1) {
+    const T* xb = x + (long long)blockIdx.z * C * HW;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const long long j = (long long)(2 * I - 1 + ky) * W + (2 * J - 1 + kx);
+        if (C == 1) {
+          const int p = pid ? pid[j] : 0;
+          acc += tab[p * 9 + ky * 3 + kx] * xb[j];
+        } else {
+          for (int ch = 0; ch < C; ++ch) acc += tab[ch * 9 + ky * 3 + kx] * xb[ch * HW + j];
+        }
+      }
+    }
+    acc = w0 * acc;
+  }
+  fc[(long long)blockIdx.z * Hc * Wc + (long long)I * Wc + J] = acc;
+}
+
+// out = add + w1 * conv_transpose2d(e, P, stride 2, pad 1)
+template <typename T>
+__global__ __launch_bounds__(256) void k_prolong(const T* __restrict__ e, int C, T* __restrict__ out,
+                                                 const T* __restrict__ add, const uint8_t* __restrict__ pidc,
+                                                 const T* __restrict__ ptab, int ntab, T w1, int Hc, int Wc) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, ptab, ntab * 9);
+  __syncthreads();
+  const int H = 2 * Hc - 1, W = 2 * Wc - 1;
+  const int x = blockIdx.x * kBX + threadIdx.x, y = blockIdx.y * kBY + threadIdx.y;
+  if (y >= H || x >= W) return;
+  const long long HWc = (long long)Hc * Wc;
+  const T* eb = e + (long long)blockIdx.z * C * HWc;
+  T acc = 0;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int ty = y + 1 - ky;
+    if (ty & 1) continue;
+    const int a = ty >> 1;
+    if (a < 0 || a >= Hc) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int tx = x + 1 - kx;
+      if (tx & 1) continue;
+      const int bb = tx >> 1;
+      if (bb < 0 || bb >= Wc) continue;
+      const long long j = (long long)a * Wc + bb;
+      if (C == 1) {
+        const int p = pidc ? pidc[j] : 0;
+        acc += tab[p * 9 + ky * 3 + kx] * eb[j];
+      } else {
+        for (int ch = 0; ch < C; ++ch) acc += tab[ch * 9 + ky * 3 + kx] * eb[ch * HWc + j];
+      }
+    }
+  }
+  const long long i = (long long)blockIdx.z * H * W + (long long)y * W + x;
+  const T v = w1 * acc;
+  out[i] = add ? add[i] + v : v;
+}
+
+// Per-block partial sums of r^2 over the interior; r = f - K u (or u itself when f == NULL).
+template <typename T>
+__global__ __launch_bounds__(256) void k_norm_partial(const T* __restrict__ u, const T* __restrict__ f,
+                                                      const uint8_t* __restrict__ pid,
+                                                      const T* __restrict__ ktab, int ntab,
+                                                      double* __restrict__ part, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  __shared__ double wsum[4];
+  if (ktab) load_table(tab, ktab, ntab * 9);
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  double s = 0.0;
+  if (r > 0 && r < H - 1 && c > 0 && c < W - 1) {
+    const long long HW = (long long)H * W;
+    const T* ub = u + blockIdx.z * HW;
+    T v;
+    if (f) {
+      T acc = 0;
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+          const long long j = (long long)(r + dr - 1) * W + (c + dc - 1);
+          const int p = pid ? pid[j] : 0;
+          acc += tab[p * 9 + dr * 3 + dc] * ub[j];
+        }
+      v = f[blockIdx.z * HW + (long long)r * W + c] - acc;
+    } else {
+      v = ub[(long long)r * W + c];
+    }
+    s = (double)v * (double)v;
+  }
+  s = wave_sum(s);
+  if (lane_id() == 0) wsum[threadIdx.y] = s;
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    const long long nb = (long long)gridDim.x * gridDim.y;
+    part[blockIdx.z * nb + (long long)blockIdx.y * gridDim.x + blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+  }
+}
+
+}  // namespace fea
+
+using namespace fea;
+
+static inline dim3 grid_for(int H, int W, int B) { return dim3((W + kBX - 1) / kBX, (H + kBY - 1) / kBY, B); }
+static inline bool bad_shape(int B, int H, int W) { return B <= 0 || H <= 0 || W <= 0 || B > 65535; }
+
+#define FEA_GENERIC_API(SUF, T)                                                                          \
+  extern "C" int fea_knet_apply_##SUF(const T* u, T* y, const uint8_t* pid, const T* ktab, int ntab, int B, \
+                                      int H, int W, void* stream) {                                      \
+    if (!u || !y || !ktab || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W)) return FEA_EINVAL; \
+    k_knet<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, y, pid, ktab, ntab, H, W); \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_split_x_##SUF(const T* x, T* xs, const uint8_t* pid, int C, int B, int H, int W,   \
+                                   void* stream) {                                                       \
+    if (!x || !xs || C < 1 || bad_shape(B, H, W)) return FEA_EINVAL;                                     \
+    k_split<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(x, xs, pid, C, H, W);       \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_jacobi_sweep_##SUF(const T* u, const T* f, T* out, const uint8_t* pid, const T* ktab, \
+                                        const T* omd, int ntab, const T* geo, long long geo_bs,          \
+                                        const T* bc, long long bc_bs, int B, int H, int W, void* stream) { \
+    if (!u || !f || !out || !ktab || !omd || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W))  \
+      return FEA_EINVAL;                                                                                 \
+    if (out == u) return FEA_EINVAL;                                                                     \
+    k_jacobi<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, f, out, pid, ktab, omd, \
+                                                                                ntab, geo, geo_bs, bc,   \
+                                                                                bc_bs, H, W);            \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_residual_##SUF(const T* u, const T* f, T* r, const uint8_t* pid, const T* ktab,    \
+                                    int ntab, int B, int H, int W, void* stream) {                       \
+    if (!u || !f || !r || !ktab || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W))            \
+      return FEA_EINVAL;                                                                                 \
+    k_residual<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, f, r, pid, ktab, ntab, \
+                                                                                  H, W);                 \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_restrict_##SUF(const T* x, int C, T* fc, const uint8_t* pid, const T* rtab, int ntab, \
+                                    T w0, int B, int H, int W, void* stream) {                           \
+    if (!x || !fc || !rtab || C < 1 || bad_shape(B, H, W) || H < 3 || W < 3 || !(H & 1) || !(W & 1))      \
+      return FEA_EINVAL;                                                                                 \
+    if ((C == 1 && (ntab < 1 || ntab > FEA_MAX_PATTERNS)) || (C > 1 && (ntab != C || C > FEA_MAX_PATTERNS))) \
+      return FEA_EINVAL;                                                                                 \
+    const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;                                                        \
+    k_restrict<T><<<grid_for(Hc, Wc, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(x, C, fc, pid, rtab,  \
+                                                                                    ntab, w0, H, W);     \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_prolong_##SUF(const T* e, int C, T* out, const T* add, const uint8_t* pidc,          \
+                                   const T* ptab, int ntab, T w1, int B, int Hc, int Wc, void* stream) { \
+    if (!e || !out || !ptab || C < 1 || bad_shape(B, Hc, Wc) || Hc < 2 || Wc < 2) return FEA_EINVAL;     \
+    if ((C == 1 && (ntab < 1 || ntab > FEA_MAX_PATTERNS)) || (C > 1 && (ntab != C || C > FEA_MAX_PATTERNS))) \
+      return FEA_EINVAL;                                                                                 \
+    k_prolong<T><<<grid_for(2 * Hc - 1, 2 * Wc - 1, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(       \
+        e, C, out, add, pidc, ptab, ntab, w1, Hc, Wc);                                                   \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,     \
+                                         int ntab, double* out, double* ws, int B, int H, int W,         \
+                                         void* stream) {                                                 \
+    if (!u || !out || !ws || bad_shape(B, H, W) || H < 3 || W < 3) return FEA_EINVAL;                     \
+    if (f && (!ktab || ntab < 1 || ntab > FEA_MAX_PATTERNS)) return FEA_EINVAL;                           \
+    const dim3 g = grid_for(H, W, B);                                                                    \
+    k_norm_partial<T><<<g, dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, f, pid, f ? ktab : nullptr, ntab, \
+                                                                      ws, H, W);                         \
+    k_norm_final<<<B, 256, 0, (hipStream_t)stream>>>(ws, (long long)g.x * g.y, out);                  \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }
+
+FEA_GENERIC_API(f32, float)
+FEA_GENERIC_API(f64, double)

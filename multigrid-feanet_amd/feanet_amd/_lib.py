@@ -1,0 +1,100 @@
+"""ctypes binding of libfeanet_hip.so (C ABI: include/feanet_hip.h).
+
+The product path has no CPU fallback: if the library is missing or no HIP device is present,
+every op raises.  `torch` is imported first so the library binds to the HIP runtime torch
+loaded (libamdhip64.so.7), not a second copy.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load)
+
+from .build import LIB
+
+ABI_VERSION = 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+
+# name -> argtypes (the _f32/_f64 pairs share a signature up to the scalar type S)
+_SIGS = {
+    "knet_apply": [P, P, P, P, I, I, I, I, P],
+    "split_x": [P, P, P, I, I, I, I, P],
+    "jacobi_sweep": [P, P, P, P, P, P, I, P, LL, P, LL, I, I, I, P],
+    "residual": [P, P, P, P, P, I, I, I, I, P],
+    "restrict": [P, I, P, P, P, I, "S", I, I, I, P],
+    "prolong": [P, I, P, P, P, P, I, "S", I, I, I, P],
+    "residual_norm": [P, P, P, P, I, P, P, I, I, I, P],
+    "mg_pack": [P, P, P, LL, P, LL, I, I, I, LL, P],
+    "mg_unpack": [P, P, I, I, I, LL, P],
+    "mg_sweep": [P, P, P, P, P, P, I, I, I, I, LL, P],
+    "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
+    "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
+    "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, LL, I, LL, P],
+    "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, LL, P],
+}
+_EXTRA = {
+    "fea_abi_version": ([], I),
+    "fea_mg_layout": ([I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
+    "fea_norm_workspace_bytes": ([I, I], ctypes.c_size_t),
+}
+
+_lib = None
+
+
+def exported_symbols():
+    """Every symbol the library must export (== every function declared in feanet_hip.h)."""
+    names = list(_EXTRA)
+    for base in _SIGS:
+        names += [f"fea_{base}_f32", f"fea_{base}_f64"]
+    return names
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        raise RuntimeError(f"feanet_amd: {LIB} is missing; run `python -m feanet_amd.build` "
+                           "(there is no CPU fallback for the HIP path)")
+    L = ctypes.CDLL(LIB)
+    for name, (args, res) in _EXTRA.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    for base, args in _SIGS.items():
+        for suf, S in (("f32", F32), ("f64", F64)):
+            fn = getattr(L, f"fea_{base}_{suf}")
+            fn.argtypes = [S if a == "S" else a for a in args]
+            fn.restype = I
+    if L.fea_abi_version() != ABI_VERSION:
+        raise RuntimeError("feanet_amd: libfeanet_hip.so ABI version mismatch; rebuild it")
+    _lib = L
+    return L
+
+
+def call(name, dtype, *args):
+    """Invoke fea_<name>_{f32,f64}; raise RuntimeError on a nonzero return (FEA_EINVAL or hipError_t)."""
+    suf = {torch.float32: "f32", torch.float64: "f64"}.get(dtype)
+    if suf is None:
+        raise TypeError(f"feanet_amd: unsupported dtype {dtype} (float32/float64 only)")
+    fn = getattr(lib(), f"fea_{name}_{suf}")
+    rc = fn(*args)
+    if rc != 0:
+        what = "invalid arguments" if rc == -1 else f"hipError_t {rc}"
+        raise RuntimeError(f"feanet_amd: fea_{name}_{suf} failed ({what})")
+
+
+def mg_layout(N, elem_size):
+    ld = I()
+    bs = LL()
+    if lib().fea_mg_layout(N, elem_size, ctypes.byref(ld), ctypes.byref(bs)) != 0:
+        raise ValueError(f"feanet_amd: unsupported level size N={N} (need N = 2^k + 1 >= 5)")
+    return ld.value, bs.value
+
+
+def norm_workspace_bytes(B, N):
+    return int(lib().fea_norm_workspace_bytes(B, N))

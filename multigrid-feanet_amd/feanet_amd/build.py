@@ -1,0 +1,48 @@
+"""Build libfeanet_hip.so (gfx950) in-tree with hipcc.
+
+The library is plain HIP C++ behind a C ABI (include/feanet_hip.h); it is loaded with ctypes
+after `import torch`, so it binds to the HIP runtime torch already loaded (same soname).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIB = os.path.join(HERE, "libfeanet_hip.so")
+SOURCES = ["generic_ops.hip", "framed_ops.hip", "coarse_tail.hip", "mg_plan.hip"]
+ARCH = os.environ.get("FEANET_ARCH", "gfx950")
+
+
+def sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(INCLUDE, "feanet_hip.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_build():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-pass-failed", f"-I{INCLUDE}", f"-I{CSRC}", *sources(), "-o", LIB + ".tmp"]
+    if verbose:
+        print("[feanet_amd.build]", " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB)

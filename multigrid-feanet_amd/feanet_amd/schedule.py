@@ -1,0 +1,81 @@
+"""Symbolic V-cycle schedule (pure host logic, no device code).
+
+One V-cycle of the reference drivers is expressed as a list of fused level steps over named
+buffers ("a", "b" ping-pong, "zero" an all-zero field).  The MultigridSolver binds the steps to
+C-ABI calls with device pointers; tests interpret the same list with the CPU oracle to show the
+fused schedule equals the reference's op sequence.
+
+Steps:
+  ("sweep", l, src, dst)               dst = J_l(src, f_l); src None means a zero initial guess
+  ("resid_restrict", l, src, vout)     f_{l+1} = w0 R(f_l - K_l src); src None: zero-guess sweep
+                                       fused first (v = omd*f_l written to vout, then restricted)
+  ("prolong_sweep", l, src, csrc, dst) dst = J_l(src + w1 P(v_{l+1}[csrc]), f_l)
+  ("prolong_add", l, src, csrc, dst)   dst = src + w1 P(v_{l+1}[csrc])
+
+Semantics reproduced:
+  * nu1 = nu2 = 1: MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372) == MultiGrid.iterate
+    (FEANet/multigrid.py:159-185): coarse levels start from zero, coarsest gets nu1 + nu2 sweeps.
+  * general nu1, nu2: Multigrid.rec_V_cycle (MM_Model_convergence.ipynb:132-148).
+  * compat="mm_interface_q2": MM_Interface_error.ipynb:132-150, whose pre-smoothing is applied to
+    grids[0] at every depth.
+"""
+
+
+def _other(b):
+    return "b" if b == "a" else "a"
+
+
+def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a"):
+    if L < 1 or nu1 < 0 or nu2 < 0:
+        raise ValueError("vcycle_schedule: need L >= 1, nu1, nu2 >= 0")
+    if compat not in (None, "mm_interface_q2"):
+        raise ValueError(f"vcycle_schedule: unknown compat mode {compat!r}")
+    steps = []
+    cur = ["zero"] * L
+    cur[0] = start
+
+    def sweep(l, zero=False):
+        dst = "a" if (zero or cur[l] == "zero") else _other(cur[l])
+        steps.append(("sweep", l, None if (zero or cur[l] == "zero") else cur[l], dst))
+        cur[l] = dst
+
+    if L == 1:
+        for _ in range(nu1 + nu2):
+            sweep(0)
+        return steps, cur[0]
+    q2 = compat == "mm_interface_q2"
+    # ---- down
+    for _ in range(nu1):
+        sweep(0)
+    steps.append(("resid_restrict", 0, cur[0], None))
+    if q2:
+        for _ in range((L - 1) * nu1):
+            sweep(0)
+    for l in range(1, L - 1):
+        if q2 or nu1 == 0:
+            cur[l] = "zero"
+            steps.append(("resid_restrict", l, "zero", None))
+        elif nu1 == 1:
+            steps.append(("resid_restrict", l, None, "a"))
+            cur[l] = "a"
+        else:
+            sweep(l, zero=True)
+            for _ in range(nu1 - 1):
+                sweep(l)
+            steps.append(("resid_restrict", l, cur[l], None))
+    # ---- coarsest
+    ncs = nu2 if q2 else nu1 + nu2
+    if ncs > 0:
+        sweep(L - 1, zero=True)
+        for _ in range(ncs - 1):
+            sweep(L - 1)
+    else:
+        cur[L - 1] = "zero"
+    # ---- up
+    for l in range(L - 2, -1, -1):
+        dst = "a" if cur[l] == "zero" else _other(cur[l])
+        steps.append(("prolong_sweep" if nu2 >= 1 else "prolong_add", l, cur[l], cur[l + 1], dst))
+        cur[l] = dst
+        for _ in range(max(nu2 - 1, 0)):
+            sweep(l)
+    return steps, cur[0]

@@ -1,0 +1,343 @@
+"""MultigridSolver: the MI355X V-cycle over solver-owned framed level buffers.
+
+`MultigridSolver` is the facade named by BASELINE.json's north star; it executes the reference's
+V-cycle (FEANet/multigrid.py MultiGrid.iterate :159-185 == M-FEANet-mg_test.ipynb MultiGrid.Step
+:27346-27372 == MM_Model_convergence.ipynb rec_V_cycle :132-148 for nu1 = nu2 = 1) with the fused
+HIP level kernels of framed_ops.hip:
+
+  down, level 0 :  nu1 sweeps               (fea_mg_sweep)
+                   residual + restriction    (fea_mg_residual_restrict)
+  down, level l :  zero-guess sweep + residual + restriction in one pass
+                   (fea_mg_residual_restrict with u = NULL)
+  coarsest      :  nu1 + nu2 sweeps from zero (no exact solve, as the reference)
+  up, level l   :  prolongation + correction + post-sweep in one pass (fea_mg_prolong_sweep)
+
+The launch sequence of one V-cycle is built once (a list of C-ABI calls with fixed device
+pointers) and replayed as a HIP graph.  Everything stays on the device; the only host syncs
+are the ones a caller asks for (e.g. `.item()` on the residual norm, as the reference drivers do).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib, mesh_setup as ms, ops
+from .schedule import vcycle_schedule
+
+
+class _Level:
+    def __init__(self, n, B, dtype, device, pid_np=None):
+        self.n = n
+        self.N = n + 1
+        esz = 4 if dtype == torch.float32 else 8
+        self.ld, self.bs = _lib.mg_layout(self.N, esz)
+        self.B = B
+        self.dtype = dtype
+        self.device = device
+        numel = B * self.bs + 256
+        self.f = torch.zeros(numel, dtype=dtype, device=device)
+        self.a = torch.zeros(numel, dtype=dtype, device=device)
+        self.b = torch.zeros(numel, dtype=dtype, device=device)
+        self.zero = None
+        self.pid = None
+        if pid_np is not None:
+            off = 128 // esz - 1
+            p = np.zeros((self.N + 2, self.ld), np.uint8)
+            p[1:self.N + 1, off:off + self.N] = pid_np
+            self.pid = torch.from_numpy(p.reshape(-1)).to(device)
+            self.pid = torch.cat([self.pid, torch.zeros(256, dtype=torch.uint8, device=device)])
+
+    def buf(self, name):
+        if name == "zero":
+            if self.zero is None:
+                self.zero = torch.zeros_like(self.a)
+            return self.zero
+        return getattr(self, name)
+
+    def view(self, t):
+        """[B, N, N] view of the interior+boundary nodes of a framed buffer (plumbing / tests)."""
+        off = 128 // t.element_size() - 1
+        return t[:self.B * self.bs].view(self.B, self.N + 2, self.ld)[:, 1:self.N + 1, off:off + self.N]
+
+
+class MultigridSolver:
+    """Geometric-multigrid V-cycle for FEANet's structured-quad FE problems on one MI355X.
+
+    Args:
+        n: fine-grid intervals per edge (N = n + 1 nodes), a power of two >= 2.
+        levels: number of levels L (default int(log2 n), the reference's choice; coarsest n/2^(L-1)).
+        problem: "poisson" (MeshSquare, one stencil) or "interface" (MeshCenterInterface, 16
+            stencils; `prop` coefficients, `shape` 0 circle / 1 rectangle inclusion).
+        dtype: torch.float32 or torch.float64.  batch: number of right-hand sides B.
+        R, P: restriction / prolongation kernels, [C, 3, 3] with C = 1 or 16 (per-pattern, the
+            learned 16-channel operators of FEANet/multigrid.py); default the bilinear kernel
+            [[1,2,1],[2,4,2],[1,2,1]]/4 for both (mg_test; == MM's 4 x full-weighting/16).
+        w: ratios (w_R, w_P) multiplying restriction/prolongation (FEANet/multigrid.py:170,178).
+        nu1, nu2: pre/post sweeps per level; the coarsest level gets nu1 + nu2 sweeps.
+        compat: None, or "mm_interface_q2" to reproduce MM_Interface_error.ipynb:141 (pre-smoothing
+            applied to the finest grid at every depth).
+        graph: replay the V-cycle as a HIP graph (default True).
+    """
+
+    def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
+                 omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
+                 nu1=1, nu2=1, compat=None, graph=True):
+        if n < 2 or (n & (n - 1)) != 0:
+            raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
+        if dtype not in (torch.float32, torch.float64):
+            raise TypeError("MultigridSolver: dtype must be torch.float32 or torch.float64")
+        self.device = torch.device(device if device is not None else "cuda")
+        ops.require_hip(torch.empty(0, device=self.device), "solver device")
+        self.n = n
+        self.L = int(math.log2(n)) if levels is None else int(levels)
+        if self.L < 1 or (n >> (self.L - 1)) < 2:
+            raise ValueError(f"MultigridSolver: {self.L} levels do not fit n={n}")
+        self.dtype = dtype
+        self.B = int(batch)
+        self.omega = omega
+        self.size = size
+        self.problem = problem
+        self.nu1, self.nu2 = int(nu1), int(nu2)
+        self.compat = compat
+        self.use_graph = graph
+        npdt = np.float32 if dtype == torch.float32 else np.float64
+        multi = problem == "interface"
+        if problem not in ("poisson", "interface"):
+            raise ValueError(f"MultigridSolver: unknown problem {problem!r}")
+        ktab = ms.stencil_table(prop if multi else None)
+        self.ntab = ktab.shape[0]
+        lin = ms.linear_transfer_kernel() / np.float32(4.0)
+        R = lin[None] if R is None else np.asarray(torch.as_tensor(R).detach().cpu().float().numpy(), np.float32)
+        P = lin[None] if P is None else np.asarray(torch.as_tensor(P).detach().cpu().float().numpy(), np.float32)
+        R = R.reshape(-1, 3, 3)
+        P = P.reshape(-1, 3, 3)
+        if multi:  # per-pattern tables cover every pattern id
+            R = np.broadcast_to(R, (self.ntab, 3, 3)) if R.shape[0] == 1 else R
+            P = np.broadcast_to(P, (self.ntab, 3, 3)) if P.shape[0] == 1 else P
+        elif R.shape[0] != 1 or P.shape[0] != 1:
+            raise ValueError("MultigridSolver: the Poisson problem has one pattern; R/P must be [1, 3, 3]")
+        w = [float(x) for x in (w.detach().cpu().tolist() if torch.is_tensor(w) else w)]
+        self.w = (w[0], w[1])
+        dev = self.device
+        self.ktab_np = ktab
+        self.ktab = torch.from_numpy(ktab.reshape(-1, 9).astype(npdt)).to(dev)
+        self.omd = torch.from_numpy(ms.omega_over_d(ktab, omega, npdt)).to(dev)
+        self.rtab = torch.from_numpy(np.ascontiguousarray(R).reshape(-1, 9).astype(npdt)).to(dev)
+        self.ptab = torch.from_numpy(np.ascontiguousarray(P).reshape(-1, 9).astype(npdt)).to(dev)
+        self.levels = []
+        for l in range(self.L):
+            nl = n >> l
+            pid = ms.interface_pattern_map(nl + 1, shape, size) if multi else None
+            self.levels.append(_Level(nl, self.B, dtype, dev, pid))
+        self.fine_pid = (torch.from_numpy(ms.interface_pattern_map(n + 1, shape, size)).to(dev) if multi else None)
+        self.ws = torch.zeros(max(1, _lib.norm_workspace_bytes(self.B, n + 1) // 8), dtype=torch.float64,
+                              device=dev)
+        self.norm_out = torch.zeros(self.B, dtype=torch.float64, device=dev)
+        self._state = "a"
+        self._plans = {}
+        self._graphs = {}
+        self._eager_runs = {}
+        self.mass = ms.mass_stencil(size / n)
+
+    # ------------------------------------------------------------------ problem data
+    @property
+    def N(self):
+        return self.n + 1
+
+    def _check_field(self, x, name):
+        ops.require_hip(x, name)
+        x = x.to(self.dtype)
+        if x.numel() == self.N * self.N:
+            x = x.reshape(1, 1, self.N, self.N).expand(self.B, 1, self.N, self.N)
+        if tuple(x.shape[-2:]) != (self.N, self.N) or x.numel() != self.B * self.N * self.N:
+            raise ValueError(f"MultigridSolver: {name} must be [{self.B}, 1, {self.N}, {self.N}]")
+        return x.reshape(self.B, 1, self.N, self.N).contiguous()
+
+    def set_rhs(self, f=None, F=None):
+        """Set the assembled right-hand side f (= FNet(F), the `forcing_term` of the reference) or
+        the nodal source F (FNet applied on the device, FEANet/model.py:49-61)."""
+        if (f is None) == (F is None):
+            raise ValueError("MultigridSolver.set_rhs: give exactly one of f (assembled) or F (source)")
+        if F is not None:
+            F = self._check_field(F, "F")
+            f = ops.conv3x3(F, torch.from_numpy(self.mass))
+        f = self._check_field(f, "f")
+        L0 = self.levels[0]
+        self._pack(f, L0.f, geo=None, bc=None, reset=False)
+
+    def set_boundary(self, bc_value=None, geometry_idx=None):
+        """Dirichlet data of the fine level (the `boundary_value` / `geometry_idx` of JacobiBlock).
+        The framed kernels implement the square geometry (geo.py:13-30); other geometries go through
+        FEANet.jacobi.JacobiBlock's generic operator."""
+        if geometry_idx is not None:
+            g = self._check_field(geometry_idx, "geometry_idx")
+            sq = torch.ones_like(g)
+            sq[..., 0, :] = 0
+            sq[..., -1, :] = 0
+            sq[..., :, 0] = 0
+            sq[..., :, -1] = 0
+            if not torch.equal(g, sq):
+                raise NotImplementedError("MultigridSolver: only the square geometry (geo.py:13-30) is fused")
+        self._bc = None if bc_value is None else self._check_field(bc_value, "boundary_value")
+
+    def _pack(self, x, dst, geo=None, bc=None, reset=True):
+        Lv = self.levels[0]
+        gp, gs = (None, 0)
+        bp, bs = (None, 0)
+        if bc is not None:
+            bp, bs = bc.data_ptr(), self.N * self.N
+        if reset:
+            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), gp, gs, bp, bs, self.B, self.N, Lv.ld,
+                      Lv.bs, ops._stream(x))
+        else:  # raw copy: geometry = all ones
+            ones = torch.ones_like(x)
+            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), ones.data_ptr(), self.N * self.N,
+                      None, 0, self.B, self.N, Lv.ld, Lv.bs, ops._stream(x))
+
+    def load(self, u0=None):
+        """Set the fine-grid iterate (reset_boundary applied: u*geo + bc, jacobi.py:27-29)."""
+        L0 = self.levels[0]
+        bc = getattr(self, "_bc", None)
+        if u0 is None:
+            u0 = torch.zeros((self.B, 1, self.N, self.N), dtype=self.dtype, device=self.device)
+        u0 = self._check_field(u0, "u0")
+        self._pack(u0, L0.a, bc=bc)
+        self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
+        self._state = "a"
+
+    def solution(self):
+        """Current fine iterate as a contiguous [B, 1, N, N] tensor."""
+        L0 = self.levels[0]
+        out = torch.empty((self.B, 1, self.N, self.N), dtype=self.dtype, device=self.device)
+        _lib.call("mg_unpack", self.dtype, L0.buf(self._state).data_ptr(), out.data_ptr(), self.B, self.N, L0.ld,
+                  L0.bs, ops._stream(out))
+        return out
+
+    def residual_norm(self):
+        """Per-sample ||(f - K u)[1:-1, 1:-1]||_2 of the current iterate (float64 device tensor [B])."""
+        L0 = self.levels[0]
+        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(),
+                  None if L0.pid is None else L0.pid.data_ptr(), self.ktab.data_ptr(), self.ntab,
+                  self.norm_out.data_ptr(), self.ws.data_ptr(), self.B, self.N, L0.ld, L0.bs,
+                  torch.cuda.current_stream(self.device).cuda_stream)
+        return self.norm_out.clone()
+
+    # ------------------------------------------------------------------ schedule
+    def _ptr(self, lvl, name):
+        return self.levels[lvl].buf(name).data_ptr()
+
+    def _build(self, start):
+        """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
+        list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
+        lv = self.levels
+        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start)
+        kt, om, nt = self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab
+        rt, pt = self.rtab.data_ptr(), self.ptab.data_ptr()
+        nr, npt = self.rtab.shape[0], self.ptab.shape[0]
+
+        def pid(l):
+            return None if lv[l].pid is None else lv[l].pid.data_ptr()
+
+        def ptr(l, name):
+            return None if name is None else self._ptr(l, name)
+
+        def geom(l):
+            return (lv[l].B, lv[l].N, lv[l].ld, lv[l].bs)
+
+        def cgeom(l):
+            return (lv[l + 1].ld, lv[l + 1].bs)
+
+        plan = []
+        for st in steps:
+            kind, l = st[0], st[1]
+            f = lv[l].f.data_ptr()
+            if kind == "sweep":
+                plan.append(("mg_sweep", (ptr(l, st[2]), f, ptr(l, st[3]), pid(l), kt, om, nt) + geom(l)))
+            elif kind == "resid_restrict":
+                plan.append(("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
+                                                      kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l)))
+            elif kind == "prolong_sweep":
+                plan.append(("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
+                                                  pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l)))
+            elif kind == "prolong_add":
+                plan.append(("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
+                                                self.w[1]) + geom(l) + cgeom(l)))
+            else:  # pragma: no cover
+                raise AssertionError(kind)
+        return plan, end
+
+    def _plan(self, start):
+        if start not in self._plans:
+            self._plans[start] = self._build(start)
+        return self._plans[start]
+
+    def _launch(self, plan):
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for name, args in plan:
+            _lib.call(name, self.dtype, *args, stream)
+
+    def vcycle(self, k=1):
+        """Run k V-cycles on the resident iterate (asynchronous; no host sync)."""
+        for _ in range(k):
+            plan, end = self._plan(self._state)
+            if not self.use_graph or self._eager_runs.get(self._state, 0) == 0:
+                self._eager_runs[self._state] = self._eager_runs.get(self._state, 0) + 1
+                self._launch(plan)
+            else:
+                g = self._graphs.get(self._state)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    s = torch.cuda.Stream(self.device)
+                    s.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.graph(g, stream=s):
+                        self._launch(plan)
+                    torch.cuda.current_stream(self.device).wait_stream(s)
+                    self._graphs[self._state] = g
+                g.replay()
+            self._state = end
+
+    def step(self, u, f):
+        """Functional form of MultiGrid.Step / MultiGrid.iterate: one V-cycle from u with rhs f,
+        returns the new fine iterate."""
+        self.set_rhs(f=f)
+        self.load(u)
+        self.vcycle()
+        return self.solution()
+
+    def solve(self, u0=None, f=None, F=None, eps=1e-6, max_cycles=100, bc_value=None):
+        """Driver loop of the reference notebooks: V-cycles until max_b ||r_b|| <= eps.  Returns
+        (u [B,1,N,N], residual history list of per-sample numpy arrays, first entry = initial)."""
+        if bc_value is not None:
+            self.set_boundary(bc_value)
+        if f is not None or F is not None:
+            self.set_rhs(f=f, F=F)
+        self.load(u0)
+        hist = [self.residual_norm().cpu().numpy()]
+        while hist[-1].max() > eps and len(hist) <= max_cycles:
+            self.vcycle()
+            hist.append(self.residual_norm().cpu().numpy())
+            if not np.all(np.isfinite(hist[-1])):
+                break
+        return self.solution(), hist
+
+    # ------------------------------------------------------------------ accounting
+    def bytes_per_vcycle(self):
+        """Algorithmic HBM bytes of one V-cycle as executed (DESIGN.md §4 accounting)."""
+        esz = 4 if self.dtype == torch.float32 else 8
+        pb = 1 if self.problem == "interface" else 0
+        total = 0
+        for name, args in self._plan(self._state)[0]:
+            B, N = args[-6:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add") else args[-4:-2]
+            nodes = B * (N - 2) ** 2
+            coarse = B * ((N + 1) // 2 - 2) ** 2
+            if name == "mg_sweep":
+                total += nodes * (esz * (3 if args[0] is not None else 2) + pb)
+            elif name == "mg_residual_restrict":
+                total += nodes * (esz * (2 if args[0] is not None else 2) + pb) + coarse * esz
+                if args[0] is None:
+                    total += nodes * esz  # v written
+            elif name == "mg_prolong_sweep":
+                total += nodes * (3 * esz + pb) + coarse * (esz + pb)
+            elif name == "mg_prolong_add":
+                total += nodes * 2 * esz + coarse * (esz + pb)
+        return total

@@ -144,9 +144,10 @@ def knet_apply(u, pid, ktab):
     pp = np.zeros((H + 2, W + 2), np.int64)
     pp[1:-1, 1:-1] = pid
     y = np.zeros((B, H, W), dt)
+    single = tab.shape[0] == 1 or not np.any(pp)
     for dr in range(3):
         for dc in range(3):
-            coef = tab[pp[dr:dr + H, dc:dc + W], dr, dc]
+            coef = tab[0, dr, dc] if single else tab[pp[dr:dr + H, dc:dc + W], dr, dc]
             y += coef * up[:, dr:dr + H, dc:dc + W]
     return y.reshape(shape)
 
@@ -179,7 +180,8 @@ def jacobi_sweep(u, f, pid, ktab, geo, bc, omega=2. / 3.):
     dt = np.asarray(u).dtype.type
     u0 = u * geo + bc
     r = f - knet_apply(u0, pid, ktab)
-    omd = omega_over_d(ktab, omega, dt)[np.asarray(pid, np.int64)]
+    omd = omega_over_d(ktab, omega, dt)
+    omd = omd[0] if len(omd) == 1 else omd[np.asarray(pid, np.int64)]
     u1 = omd * r + u0
     return u1 * geo + bc
 
@@ -205,7 +207,7 @@ def restrict(r, pid, rtab, w0=1.0):
         for kx in range(3):
             rs = r3[:, 1 + ky:1 + ky + 2 * (Hc - 2):2, 1 + kx:1 + kx + 2 * (Wc - 2):2]
             ps = pid[1 + ky:1 + ky + 2 * (Hc - 2):2, 1 + kx:1 + kx + 2 * (Wc - 2):2]
-            acc += tab[ps, ky, kx] * rs
+            acc += (tab[0, ky, kx] if tab.shape[0] == 1 else tab[ps, ky, kx]) * rs
     out = np.zeros((B, Hc, Wc), dt)
     out[:, 1:-1, 1:-1] = acc
     if w0 != 1.0:
@@ -227,7 +229,8 @@ def prolong(e, pidc, ptab, w1=1.0):
     outp = np.zeros((B, H + 2, W + 2), dt)
     for ky in range(3):
         for kx in range(3):
-            outp[:, ky:ky + 2 * Hc:2, kx:kx + 2 * Wc:2] += tab[pidc, ky, kx] * e3
+            outp[:, ky:ky + 2 * Hc:2, kx:kx + 2 * Wc:2] += (tab[0, ky, kx] if tab.shape[0] == 1 else
+                                                             tab[pidc, ky, kx]) * e3
     out = outp[:, 1:-1, 1:-1]
     if w1 != 1.0:
         out = (dt(w1) * out).astype(dt)

@@ -1,0 +1,107 @@
+"""The fused V-cycle schedule (feanet_amd.schedule) is the reference's V-cycle: interpret the
+symbolic step list with the CPU oracle's operators and compare with the oracle's own drivers
+(MultiGrid.Step / rec_V_cycle / the MM_Interface Q2 variant).  CPU only (host logic)."""
+import numpy as np
+import pytest
+
+from feanet_amd.schedule import vcycle_schedule
+from oracle import feanet_oracle as orc
+
+
+def interpret(mg, steps, v, f, compat=None):
+    """Execute a symbolic schedule with oracle ops. `compat` selects the oracle's transfer flavour."""
+    L = mg.L
+    lv = mg.levels
+    dt = mg.dtype
+    B = v.shape[0]
+    bufs = [dict() for _ in range(L)]
+    bufs[0]["a"] = v
+    fs = [None] * L
+    fs[0] = f
+
+    def get(l, name):
+        if name == "zero":
+            return np.zeros((B, lv[l].N, lv[l].N), dt)
+        return bufs[l][name]
+
+    for st in steps:
+        kind, l = st[0], st[1]
+        if kind == "sweep":
+            src = np.zeros((B, lv[l].N, lv[l].N), dt) if st[2] is None else get(l, st[2])
+            bufs[l][st[3]] = lv[l].sweep(src, fs[l])
+        elif kind == "resid_restrict":
+            if st[2] is None:
+                src = lv[l].sweep(np.zeros((B, lv[l].N, lv[l].N), dt), fs[l])
+                bufs[l][st[3]] = src
+            else:
+                src = get(l, st[2])
+            r = fs[l] - lv[l].K(src)
+            if compat == "mm":
+                fs[l + 1] = mg._mm_restrict(r)
+            else:
+                fs[l + 1] = orc.restrict(r, lv[l].pid, mg.rtab, mg.w[0])
+        elif kind in ("prolong_sweep", "prolong_add"):
+            src = get(l, st[2])
+            e = get(l + 1, st[3])
+            if compat == "mm":
+                corr = orc.bilinear_upsample(e) * lv[l].geo + lv[l].bc
+            else:
+                corr = orc.prolong(e, lv[l + 1].pid, mg.ptab, mg.w[1])
+            x = src + corr
+            bufs[l][st[4]] = lv[l].sweep(x, fs[l]) if kind == "prolong_sweep" else x
+    return bufs
+
+
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("L", [1, 2, 3, 5])
+def test_step_schedule_equals_reference_step(problem, L):
+    n = 32
+    rng = np.random.default_rng(L)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    steps, end = vcycle_schedule(L, 1, 1)
+    out = interpret(mg, steps, v, f)[0][end]
+    ref = mg.step(v, f)
+    np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("nu", [(1, 1), (0, 1), (1, 0), (2, 1), (1, 2), (2, 2), (0, 2), (2, 0), (3, 1)])
+def test_nu_schedules_equal_rec_vcycle(nu):
+    n = 32
+    rng = np.random.default_rng(sum(nu))
+    mg = orc.OracleMultigrid(n, "poisson", np.float64)
+    v = rng.standard_normal((1, n + 1, n + 1))
+    f = rng.standard_normal((1, n + 1, n + 1))
+    steps, end = vcycle_schedule(mg.L, *nu)
+    out = interpret(mg, steps, v, f, compat="mm")[0][end]
+    ref = mg.rec_vcycle(v, f, *nu)
+    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_q2_schedule_equals_mm_interface():
+    n = 32
+    rng = np.random.default_rng(7)
+    mg = orc.OracleMultigrid(n, "interface", np.float64)
+    v = rng.standard_normal((1, n + 1, n + 1))
+    f = rng.standard_normal((1, n + 1, n + 1))
+    steps, end = vcycle_schedule(mg.L, 1, 1, compat="mm_interface_q2")
+    out = interpret(mg, steps, v, f, compat="mm")[0][end]
+    ref = mg.rec_vcycle(v, f, 1, 1, compat_q2=True)
+    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_schedule_shape_and_buffers():
+    steps, end = vcycle_schedule(12, 1, 1)
+    kinds = [s[0] for s in steps]
+    # 1 fine sweep, 11 residual-restrictions, 2 coarsest sweeps, 11 fused prolong+sweep
+    assert kinds.count("sweep") == 3 and kinds.count("resid_restrict") == 11
+    assert kinds.count("prolong_sweep") == 11 and end == "a"
+    for s in steps:  # no step reads and writes the same buffer
+        if s[0] == "sweep":
+            assert s[2] != s[3]
+        if s[0].startswith("prolong"):
+            assert s[2] != s[4]
+    # odd number of fine writes alternates the resident buffer
+    steps, end = vcycle_schedule(4, 2, 1)
+    assert end == "b"
