@@ -185,6 +185,24 @@ int fea_mg_residual_norm_f32(const float* u, const float* f, const uint8_t* pid,
 int fea_mg_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
                              double* out, double* ws, int B, int N, int ld, long long bstride, void* stream);
 
+/* The whole coarse end of the V-cycle (levels t..t+nlev-1, N_t = 2^k + 1 <= 65) in ONE launch,
+ * one 1024-thread workgroup per sample, every level resident in LDS.  Input f_t and output v_t
+ * are framed level-t buffers (ld_t, bs_t); v_t's interior is written.  The sub-cycle starts from a
+ * zero guess: nu1 pre-sweeps per level (none if q2), nu1+nu2 (q2: nu2) sweeps on the coarsest,
+ * prolongation + correction + nu2 post-sweeps (FEANet/multigrid.py:165-183 below level t).
+ * pid_levels: the nlev compact N_k x N_k uint8 pattern maps concatenated (NULL when ntab == 1);
+ * rtab/ptab hold ntab kernels (broadcast single kernels on the host). */
+int fea_mg_coarse_tail_f32(const float* f_t, float* v_t, int Nt, int nlev, int ld_t, long long bs_t,
+                           const uint8_t* pid_levels, const float* ktab, const float* omd, int ntab,
+                           const float* rtab, const float* ptab, float w0, float w1, int nu1, int nu2, int q2,
+                           int B, void* stream);
+int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Nt, int nlev, int ld_t, long long bs_t,
+                           const uint8_t* pid_levels, const double* ktab, const double* omd, int ntab,
+                           const double* rtab, const double* ptab, double w0, double w1, int nu1, int nu2,
+                           int q2, int B, void* stream);
+/* LDS bytes the coarse tail needs for (Nt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
+size_t fea_mg_coarse_tail_lds_bytes(int Nt, int nlev, int elem_size, int multi);
+
 #ifdef __cplusplus
 }
 #endif

@@ -110,32 +110,53 @@ struct PRow {  // LDS table offsets (pattern * kTabStride) for the same columns
   int a[V + 3];
 };
 
-// Load one row segment (+ halos) of a framed field.  `rp` points at element (r, c0) of the strip.
+// Rows are loaded in two halves so a load can be issued one iteration ahead of its use:
+// raw_*() issues the 16-byte vector load of the lane's columns plus the 16-byte halo load
+// (lane 0: columns c0-V..c0-1, lane 63: c0+SW..), finish() builds the window row with DPP.
 template <typename T, int V>
-__device__ __forceinline__ Row<T, V> load_row(const T* __restrict__ rp, int lane) {
-  Row<T, V> w;
+struct RawRow {
   T x[V], h[V];
-  vload<T, V>(rp + V * lane, x);
-  vload<T, V>(rp + (lane < 32 ? -V : kWave * V), h);  // lane 0: columns c0-V..c0-1; lane 63: c0+SW..
+};
+template <int V>
+struct RawP {
+  int x[V], h[V];
+};
+
+template <typename T, int V>
+__device__ __forceinline__ RawRow<T, V> raw_row(const T* __restrict__ rp, int lane) {
+  RawRow<T, V> r;
+  vload<T, V>(rp + V * lane, r.x);
+  vload<T, V>(rp + (lane < 32 ? -V : kWave * V), r.h);
+  return r;
+}
+
+template <typename T, int V>
+__device__ __forceinline__ Row<T, V> finish(const RawRow<T, V>& r) {
+  Row<T, V> w;
 #pragma unroll
-  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k];
-  w.a[0] = shr1(x[V - 1], h[V - 1]);
-  w.a[V + 1] = shl1(x[0], h[0]);
-  w.a[V + 2] = shl1(x[1 % V], h[1 % V]);
+  for (int k = 0; k < V; ++k) w.a[k + 1] = r.x[k];
+  w.a[0] = shr1(r.x[V - 1], r.h[V - 1]);
+  w.a[V + 1] = shl1(r.x[0], r.h[0]);
+  w.a[V + 2] = shl1(r.x[1 % V], r.h[1 % V]);
   return w;
 }
 
 template <int V>
-__device__ __forceinline__ PRow<V> load_prow(const uint8_t* __restrict__ pp, int lane) {
+__device__ __forceinline__ RawP<V> raw_prow(const uint8_t* __restrict__ pp, int lane) {
+  RawP<V> r;
+  pload<V>(pp + V * lane, r.x);
+  pload<V>(pp + (lane < 32 ? -V : kWave * V), r.h);
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ PRow<V> finish(const RawP<V>& r) {
   PRow<V> w;
-  int x[V], h[V];
-  pload<V>(pp + V * lane, x);
-  pload<V>(pp + (lane < 32 ? -V : kWave * V), h);
 #pragma unroll
-  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * kTabStride;
-  w.a[0] = shr1(x[V - 1], h[V - 1]) * kTabStride;
-  w.a[V + 1] = shl1(x[0], h[0]) * kTabStride;
-  w.a[V + 2] = shl1(x[1 % V], h[1 % V]) * kTabStride;
+  for (int k = 0; k < V; ++k) w.a[k + 1] = r.x[k] * kTabStride;
+  w.a[0] = shr1(r.x[V - 1], r.h[V - 1]) * kTabStride;
+  w.a[V + 1] = shl1(r.x[0], r.h[0]) * kTabStride;
+  w.a[V + 2] = shl1(r.x[1 % V], r.h[1 % V]) * kTabStride;
   return w;
 }
 
@@ -190,6 +211,7 @@ struct MgArgs {
   int Nc, ldc;
   long long bsc;
   int nstrips, ntr;  // strips per row, row tasks per sample
+  int rb;            // fine rows per row task (even)
 };
 
 struct TaskId {
@@ -226,6 +248,17 @@ __device__ __forceinline__ void load_tables(T* tab, const T* ktab, const T* omd,
     }
 }
 
+template <typename T, int V>
+__device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int N) {
+  if (cl + V - 1 <= N - 2) {
+    vstore<T, V>(p, o);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k)
+      if (cl + k <= N - 2) p[k] = o[k];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Kernel A: interior Jacobi sweep  out = J(u, f);  ZERO: u == 0  ->  out = omd * f
 // ---------------------------------------------------------------------------
@@ -243,10 +276,9 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   const int lane = lane_id();
   const int N = g.N;
   const int c0 = 1 + id.s * F::SW;
-  const int r0 = 1 + id.t * kRB;
-  const int r1 = min(r0 + kRB, N - 1);
+  const int r0 = 1 + id.t * g.rb;
+  const int r1 = min(r0 + g.rb, N - 1);
   const int cl = c0 + V * lane;  // first own column
-  const bool full = cl + V - 1 <= N - 2;
   T ks[9];
   T om = 0;
   if constexpr (!MULTI) {
@@ -261,57 +293,58 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   T* __restrict__ ob = g.out + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;  // pattern maps: one per mesh
   const int ld = g.ld;
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
 
   if constexpr (ZERO) {
     for (int r = r0; r < r1; ++r) {
-      const long long ro = (long long)(r + 1) * ld + V * lane;
+      const long long ro = rowo(r) + V * lane;
       T fv[V], o[V];
       vload<T, V>(fb + ro, fv);
       int pv[V];
       if constexpr (MULTI) pload<V>(pb + ro, pv);
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = (MULTI ? tab[pv[k] * kTabStride + 9] : om) * fv[k];
-      if (full) {
-        vstore<T, V>(ob + ro, o);
-      } else {
-#pragma unroll
-        for (int k = 0; k < V; ++k)
-          if (cl + k <= N - 2) ob[ro + k] = o[k];
-      }
+      store_masked<T, V>(ob + ro, o, cl, N);
     }
-    return;
   } else {
-    Row<T, V> w0 = load_row<T, V>(ub + (long long)r0 * ld, lane);
-    Row<T, V> w1 = load_row<T, V>(ub + (long long)(r0 + 1) * ld, lane);
+    Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
+    Row<T, V> w1 = finish(raw_row<T, V>(ub + rowo(r0), lane));
+    RawRow<T, V> nx = raw_row<T, V>(ub + rowo(r0 + 1), lane);
+    T fx[V];
+    vload<T, V>(fb + rowo(r0) + V * lane, fx);
     PRow<V> p0{}, p1{}, p2{};
+    RawP<V> px{};
     if constexpr (MULTI) {
-      p0 = load_prow<V>(pb + (long long)r0 * ld, lane);
-      p1 = load_prow<V>(pb + (long long)(r0 + 1) * ld, lane);
+      p0 = finish(raw_prow<V>(pb + rowo(r0 - 1), lane));
+      p1 = finish(raw_prow<V>(pb + rowo(r0), lane));
+      px = raw_prow<V>(pb + rowo(r0 + 1), lane);
     }
     for (int r = r0; r < r1; ++r) {
-      const long long ro = (long long)(r + 1) * ld;
-      const Row<T, V> w2 = load_row<T, V>(ub + ro + ld, lane);
-      if constexpr (MULTI) p2 = load_prow<V>(pb + ro + ld, lane);
-      T fv[V], o[V];
-      vload<T, V>(fb + ro + V * lane, fv);
+      // issue next iteration's loads before this row's arithmetic
+      const RawRow<T, V> nn = raw_row<T, V>(ub + rowo(r + 2), lane);
+      T fn[V];
+      vload<T, V>(fb + rowo(r + 1) + V * lane, fn);
+      RawP<V> pn{};
+      if constexpr (MULTI) pn = raw_prow<V>(pb + rowo(r + 2), lane);
+      const Row<T, V> w2 = finish(nx);
+      if constexpr (MULTI) p2 = finish(px);
+      T o[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const T acc = kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
         const T omk = MULTI ? tab[p1.a[k + 1] + 9] : om;
-        o[k] = omk * (fv[k] - acc) + w1.a[k + 1];
+        o[k] = omk * (fx[k] - acc) + w1.a[k + 1];
       }
-      if (full) {
-        vstore<T, V>(ob + ro + V * lane, o);
-      } else {
-#pragma unroll
-        for (int k = 0; k < V; ++k)
-          if (cl + k <= N - 2) ob[ro + V * lane + k] = o[k];
-      }
+      store_masked<T, V>(ob + rowo(r) + V * lane, o, cl, N);
       w0 = w1;
       w1 = w2;
+      nx = nn;
+#pragma unroll
+      for (int k = 0; k < V; ++k) fx[k] = fn[k];
       if constexpr (MULTI) {
         p0 = p1;
         p1 = p2;
+        px = pn;
       }
     }
   }
@@ -337,8 +370,8 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   const int lane = lane_id();
   const int N = g.N, Nc = g.Nc;
   const int c0 = 1 + id.s * F::SW;
-  const int I0 = 1 + id.t * (kRB / 2);
-  const int I1 = min(I0 + kRB / 2, Nc - 1);
+  const int I0 = 1 + id.t * (g.rb / 2);
+  const int I1 = min(I0 + g.rb / 2, Nc - 1);
   const int cl = c0 + V * lane;
   T ks[9], rs[9];
   T om = 0;
@@ -368,19 +401,29 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   const int bc0 = (c0 + 1) / 2;  // coarse column of lane 0's first output
   T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
   const int Jl = bc0 + Q * lane;
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
 
-  // one "window row": the field used by K (u, or v = omd*f in ZERO mode), plus the raw f row
-  // (ZERO mode: the same load) and pattern offsets.
+  // a window row: the field K acts on (u, or v = omd*f in ZERO mode), the f row, pattern offsets
+  struct RawW {
+    RawRow<T, V> u, f;
+    RawP<V> p;
+  };
   struct WRow {
-    Row<T, V> u;
-    Row<T, V> f;
+    Row<T, V> u, f;
     PRow<V> p;
   };
-  auto load_w = [&](int y) {
+  auto raw_w = [&](int y) {
+    RawW w;
+    const long long ro = rowo(y);
+    if constexpr (MULTI) w.p = raw_prow<V>(pb + ro, lane);
+    w.f = raw_row<T, V>(fb + ro, lane);
+    if constexpr (!ZERO) w.u = raw_row<T, V>(ub + ro, lane);
+    return w;
+  };
+  auto fin_w = [&](const RawW& r, int y) {
     WRow w;
-    const long long ro = (long long)(y + 1) * ld;
-    if constexpr (MULTI) w.p = load_prow<V>(pb + ro, lane);
-    w.f = load_row<T, V>(fb + ro, lane);
+    if constexpr (MULTI) w.p = finish(r.p);
+    w.f = finish(r.f);
     if constexpr (ZERO) {
       const bool rin = y >= 1 && y <= N - 2;
 #pragma unroll
@@ -389,11 +432,10 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
         w.u.a[j] = (rin && cin[j]) ? omj * w.f.a[j] : T(0);
       }
     } else {
-      w.u = load_row<T, V>(ub + ro, lane);
+      w.u = finish(r.u);
     }
     return w;
   };
-  // residual at own columns k = 0..V of the centre row (f at those columns from the f row)
   auto resid = [&](const WRow& a, const WRow& b, const WRow& c, T (&r)[V + 1]) {
 #pragma unroll
     for (int k = 0; k <= V; ++k) r[k] = b.f.a[k + 1] - kapply<T, V, MULTI>(a.u, b.u, c.u, a.p, b.p, c.p, k, ks, tab);
@@ -402,41 +444,36 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     if constexpr (ZERO) {
       const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Nc - 1) && y <= N - 2;
       if (own) {
-        T* vp = vb + (long long)(y + 1) * ld + V * lane;
-        if (cl + V - 1 <= N - 2) {
-          T o[V];
+        T o[V];
 #pragma unroll
-          for (int k = 0; k < V; ++k) o[k] = w.u.a[k + 1];
-          vstore<T, V>(vp, o);
-        } else {
-#pragma unroll
-          for (int k = 0; k < V; ++k)
-            if (cl + k <= N - 2) vp[k] = w.u.a[k + 1];
-        }
+        for (int k = 0; k < V; ++k) o[k] = w.u.a[k + 1];
+        store_masked<T, V>(vb + rowo(y) + V * lane, o, cl, N);
       }
     }
   };
 
   const int y0 = 2 * I0 - 1;
-  WRow W0 = load_w(y0 - 1);
-  WRow W1 = load_w(y0);
-  WRow W2 = load_w(y0 + 1);
+  WRow W0 = fin_w(raw_w(y0 - 1), y0 - 1);
+  WRow W1 = fin_w(raw_w(y0), y0);
+  WRow W2 = fin_w(raw_w(y0 + 1), y0 + 1);
+  RawW n1 = raw_w(2 * I0 + 1), n2 = raw_w(2 * I0 + 2);
   T Ra[V + 1], Rb[V + 1], Rc[V + 1];
   PRow<V> Pa = W1.p, Pb, Pc;
   resid(W0, W1, W2, Ra);
   store_v(y0, W1);
   for (int I = I0; I < I1; ++I) {
+    const RawW m1 = raw_w(2 * I + 3), m2 = raw_w(2 * I + 4);  // next coarse row's fine rows
     // fine row 2I
     W0 = W1;
     W1 = W2;
-    W2 = load_w(2 * I + 1);
+    W2 = fin_w(n1, 2 * I + 1);
     resid(W0, W1, W2, Rb);
     Pb = W1.p;
     store_v(2 * I, W1);
     // fine row 2I+1
     W0 = W1;
     W1 = W2;
-    W2 = load_w(2 * I + 2);
+    W2 = fin_w(n2, 2 * I + 2);
     resid(W0, W1, W2, Rc);
     Pc = W1.p;
     store_v(2 * I + 1, W1);
@@ -479,6 +516,8 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
     Pa = Pc;
+    n1 = m1;
+    n2 = m2;
   }
 }
 
@@ -491,28 +530,41 @@ struct CRow {  // coarse row at coarse columns b_base-1 .. b_base+V/2 (V/2+2 val
   T e[V / 2 + 2];
   int o[V / 2 + 2];
 };
+template <typename T, int V>
+struct RawC {
+  T x[V / 2];
+  T h;
+  int px[V / 2];
+  int ph;
+};
 
 template <typename T, int V, bool MULTI>
-__device__ __forceinline__ CRow<T, V> load_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp,
-                                                int lane) {
+__device__ __forceinline__ RawC<T, V> raw_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp, int lane) {
+  constexpr int Q = V / 2;
+  RawC<T, V> c;
+  vload<T, Q>(ep + Q * lane, c.x);
+  c.h = ep[lane < 32 ? -1 : kWave * Q];
+  if constexpr (MULTI) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c.px[q] = pp[Q * lane + q];
+    c.ph = pp[lane < 32 ? -1 : kWave * Q];
+  }
+  return c;
+}
+
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ CRow<T, V> finish_c(const RawC<T, V>& r) {
   constexpr int Q = V / 2;
   CRow<T, V> c;
-  T x[Q];
-  vload<T, Q>(ep + Q * lane, x);
-  const T h = ep[lane < 32 ? -1 : kWave * Q];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) c.e[q + 1] = x[q];
-  c.e[0] = shr1(x[Q - 1], h);
-  c.e[Q + 1] = shl1(x[0], h);
+  for (int q = 0; q < Q; ++q) c.e[q + 1] = r.x[q];
+  c.e[0] = shr1(r.x[Q - 1], r.h);
+  c.e[Q + 1] = shl1(r.x[0], r.h);
   if constexpr (MULTI) {
-    int px[Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) px[q] = pp[Q * lane + q];
-    const int ph = pp[lane < 32 ? -1 : kWave * Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) c.o[q + 1] = px[q] * kTabStride;
-    c.o[0] = shr1(px[Q - 1], ph) * kTabStride;
-    c.o[Q + 1] = shl1(px[0], ph) * kTabStride;
+    for (int q = 0; q < Q; ++q) c.o[q + 1] = r.px[q] * kTabStride;
+    c.o[0] = shr1(r.px[Q - 1], r.ph) * kTabStride;
+    c.o[Q + 1] = shl1(r.px[0], r.ph) * kTabStride;
   }
   return c;
 }
@@ -553,7 +605,6 @@ template <typename T, bool MULTI, bool SWEEP>
 __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
-  constexpr int Q = V / 2;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
   __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
   if constexpr (MULTI) {
@@ -564,12 +615,11 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N;
+  const int N = g.N, Nc = g.Nc;
   const int c0 = 1 + id.s * F::SW;
-  const int r0 = 1 + id.t * kRB;  // odd
-  const int r1 = min(r0 + kRB, N - 1);
+  const int r0 = 1 + id.t * g.rb;  // odd
+  const int r1 = min(r0 + g.rb, N - 1);
   const int cl = c0 + V * lane;
-  const bool full = cl + V - 1 <= N - 2;
   T ks[9], ps[9];
   T om = 0;
   if constexpr (!MULTI) {
@@ -592,21 +642,28 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const long long pcoff = F::OFF + bc0;
   const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + pcoff;
   const uint8_t* __restrict__ pcb = MULTI ? g.pidc + pcoff : nullptr;
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
+  auto crowo = [&](int a) -> long long { return (long long)(min(a, Nc) + 1) * ldc; };
 
-  auto crow = [&](int a) { return load_crow<T, V, MULTI>(eb + (long long)(a + 1) * ldc, MULTI ? pcb + (long long)(a + 1) * ldc : nullptr, lane); };
-  auto urow = [&](int y) { return load_row<T, V>(ub + (long long)(y + 1) * ld, lane); };
-  auto prow = [&](int y) {
-    PRow<V> p{};
-    if constexpr (MULTI && SWEEP) p = load_prow<V>(pb + (long long)(y + 1) * ld, lane);
+  auto rc = [&](int a) { return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane); };
+  auto ru = [&](int y) { return raw_row<T, V>(ub + rowo(y), lane); };
+  auto rp = [&](int y) {
+    RawP<V> p{};
+    if constexpr (MULTI && SWEEP) p = raw_prow<V>(pb + rowo(y), lane);
     return p;
   };
+  auto fp = [&](const RawP<V>& r) {
+    PRow<V> p{};
+    if constexpr (MULTI && SWEEP) p = finish(r);
+    return p;
+  };
+  auto rf = [&](int y, T (&fv)[V]) {
+    if constexpr (SWEEP) vload<T, V>(fb + rowo(y) + V * lane, fv);
+  };
   auto emit = [&](int y, const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
-                  const PRow<V>& pbb, const PRow<V>& pc) {
-    const long long ro = (long long)(y + 1) * ld + V * lane;
+                  const PRow<V>& pbb, const PRow<V>& pc, const T (&fv)[V]) {
     T o[V];
     if constexpr (SWEEP) {
-      T fv[V];
-      vload<T, V>(fb + ro, fv);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const T acc = kapply<T, V, MULTI>(a, b, c, pa, pbb, pc, k, ks, tab);
@@ -617,40 +674,59 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = b.a[k + 1];
     }
-    if (full) {
-      vstore<T, V>(ob + ro, o);
-    } else {
-#pragma unroll
-      for (int k = 0; k < V; ++k)
-        if (cl + k <= N - 2) ob[ro + k] = o[k];
-    }
+    store_masked<T, V>(ob + rowo(y) + V * lane, o, cl, N);
   };
 
   // window rows r0-1 (even, coarse a0) and r0 (odd, coarse a0, a0+1)
   const int a0 = (r0 - 1) / 2;
-  CRow<T, V> C0 = crow(a0), C1 = crow(a0 + 1);
-  Row<T, V> Vp = urow(r0 - 1), Vc = urow(r0);
+  CRow<T, V> C0 = finish_c<T, V, MULTI>(rc(a0));
+  CRow<T, V> C1 = finish_c<T, V, MULTI>(rc(a0 + 1));
+  Row<T, V> Vp = finish(ru(r0 - 1)), Vc = finish(ru(r0));
   correct_even<T, V, MULTI>(Vp, C0, w1, ps, ptb);
   correct_odd<T, V, MULTI>(Vc, C0, C1, w1, ps, ptb);
-  PRow<V> Pp = prow(r0 - 1), Pc = prow(r0);
+  PRow<V> Pp = fp(rp(r0 - 1)), Pc = fp(rp(r0));
+  // prefetched for the first iteration: fine rows r0+1, r0+2, coarse row a0+2, f rows r0, r0+1
+  RawRow<T, V> nU1 = ru(r0 + 1), nU2 = ru(r0 + 2);
+  RawC<T, V> nC = rc(a0 + 2);
+  RawP<V> nP1 = rp(r0 + 1), nP2 = rp(r0 + 2);
+  T f0[V], f1[V];
+  rf(r0, f0);
+  rf(r0 + 1, f1);
   for (int y = r0; y < r1; y += 2) {
+    // next iteration's loads first
+    const RawRow<T, V> mU1 = ru(y + 3), mU2 = ru(y + 4);
+    const RawC<T, V> mC = rc((y + 5) / 2);
+    const RawP<V> mP1 = rp(y + 3), mP2 = rp(y + 4);
+    T g0[V], g1[V];
+    rf(y + 2, g0);
+    rf(y + 3, g1);
     // row y+1 (even, coarse (y+1)/2 = C1)
-    Row<T, V> Vn = urow(y + 1);
+    Row<T, V> Vn = finish(nU1);
     correct_even<T, V, MULTI>(Vn, C1, w1, ps, ptb);
-    PRow<V> Pn = prow(y + 1);
-    emit(y, Vp, Vc, Vn, Pp, Pc, Pn);
+    const PRow<V> Pn = fp(nP1);
+    emit(y, Vp, Vc, Vn, Pp, Pc, Pn, f0);
     if (y + 1 < r1) {
       // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
-      const CRow<T, V> C2 = crow((y + 3) / 2);
-      Row<T, V> Vnn = urow(y + 2);
+      const CRow<T, V> C2 = finish_c<T, V, MULTI>(nC);
+      Row<T, V> Vnn = finish(nU2);
       correct_odd<T, V, MULTI>(Vnn, C1, C2, w1, ps, ptb);
-      PRow<V> Pnn = prow(y + 2);
-      emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn);
+      const PRow<V> Pnn = fp(nP2);
+      emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn, f1);
       Vp = Vn;
       Vc = Vnn;
       Pp = Pn;
       Pc = Pnn;
       C1 = C2;
+    }
+    nU1 = mU1;
+    nU2 = mU2;
+    nC = mC;
+    nP1 = mP1;
+    nP2 = mP2;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      f0[k] = g0[k];
+      f1[k] = g1[k];
     }
   }
 }
@@ -672,8 +748,8 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
   const int lane = lane_id();
   const int N = g.N;
   const int c0 = 1 + id.s * F::SW;
-  const int r0 = 1 + id.t * kRB;
-  const int r1 = min(r0 + kRB, N - 1);
+  const int r0 = 1 + id.t * g.rb;
+  const int r1 = min(r0 + g.rb, N - 1);
   const int cl = c0 + V * lane;
   T ks[9];
   if constexpr (!MULTI) {
@@ -686,20 +762,26 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
   const T* __restrict__ fb = g.f + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
   const int ld = g.ld;
-  Row<T, V> w0 = load_row<T, V>(ub + (long long)r0 * ld, lane);
-  Row<T, V> w1 = load_row<T, V>(ub + (long long)(r0 + 1) * ld, lane);
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
+  Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
+  Row<T, V> w1 = finish(raw_row<T, V>(ub + rowo(r0), lane));
+  RawRow<T, V> nx = raw_row<T, V>(ub + rowo(r0 + 1), lane);
   PRow<V> p0{}, p1{}, p2{};
+  RawP<V> px{};
   if constexpr (MULTI) {
-    p0 = load_prow<V>(pb + (long long)r0 * ld, lane);
-    p1 = load_prow<V>(pb + (long long)(r0 + 1) * ld, lane);
+    p0 = finish(raw_prow<V>(pb + rowo(r0 - 1), lane));
+    p1 = finish(raw_prow<V>(pb + rowo(r0), lane));
+    px = raw_prow<V>(pb + rowo(r0 + 1), lane);
   }
   double s = 0.0;
   for (int r = r0; r < r1; ++r) {
-    const long long ro = (long long)(r + 1) * ld;
-    const Row<T, V> w2 = load_row<T, V>(ub + ro + ld, lane);
-    if constexpr (MULTI) p2 = load_prow<V>(pb + ro + ld, lane);
+    const RawRow<T, V> nn = raw_row<T, V>(ub + rowo(r + 2), lane);
+    RawP<V> pn{};
+    if constexpr (MULTI) pn = raw_prow<V>(pb + rowo(r + 2), lane);
     T fv[V];
-    vload<T, V>(fb + ro + V * lane, fv);
+    vload<T, V>(fb + rowo(r) + V * lane, fv);
+    const Row<T, V> w2 = finish(nx);
+    if constexpr (MULTI) p2 = finish(px);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T rr = fv[k] - kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
@@ -707,9 +789,11 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
     }
     w0 = w1;
     w1 = w2;
+    nx = nn;
     if constexpr (MULTI) {
       p0 = p1;
       p1 = p2;
+      px = pn;
     }
   }
   s = wave_sum(s);
@@ -751,14 +835,24 @@ static inline bool mg_n_ok(int N) {
   return (n & (n - 1)) == 0;
 }
 
+// Rows per wave task: the largest even count (<= kRB) that still gives >= kTargetWaves waves,
+// so small levels are spread over the chip instead of being marched row by row by a few waves.
+constexpr int kTargetWaves = 4096;
+static inline int pick_rb(int B, int nstrips, int rows) {
+  for (int rb = kRB; rb > 2; rb /= 2)
+    if ((long long)B * nstrips * div_up(rows, rb) >= kTargetWaves) return rb;
+  return 2;
+}
+
 template <typename T>
-static MgArgs<T> mg_args(int N, int ld, long long bs) {
+static MgArgs<T> mg_args(int N, int ld, long long bs, int B) {
   MgArgs<T> g{};
   g.N = N;
   g.ld = ld;
   g.bs = bs;
   g.nstrips = mg_nstrips<T>(N);
-  g.ntr = div_up(N - 2, kRB);
+  g.rb = pick_rb(B, g.nstrips, N - 2);
+  g.ntr = div_up(N - 2, g.rb);
   return g;
 }
 
@@ -813,7 +907,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
                                     const T* omd, int ntab, int B, int N, int ld, long long bs, void* stream) { \
     if (!f || !out || !ktab || !omd || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                 \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || out == u) return FEA_EINVAL;             \
-    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
     g.u = u; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;                   \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
@@ -837,10 +931,10 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
     if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;                                                      \
     if (!u && (!v_out || !omd)) return FEA_EINVAL;                                                           \
-    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
     g.u = u; g.f = f; g.out = fc; g.out2 = v_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
     g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;                           \
-    g.ntr = div_up(Nc - 2, kRB / 2);                                                                         \
+    g.ntr = div_up(Nc - 2, g.rb / 2);                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
@@ -866,7 +960,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
       return FEA_EINVAL;                                                                                     \
     const bool multi = nptab > 1 || (sweep && ntab > 1);                                                     \
     if (multi && ((sweep && (!pid || ntab == 1)) || !pidc || nptab == 1)) return FEA_EINVAL;                 \
-    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
     g.u = u; g.ec = ec; g.f = f; g.out = out; g.pid = pid; g.pidc = pidc; g.ktab = ktab; g.omd = omd;         \
     g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;            \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
@@ -898,7 +992,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
                                             long long bs, void* stream) {                                    \
     if (!u || !f || !ktab || !out || !ws || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;            \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
-    MgArgs<T> g = mg_args<T>(N, ld, bs);                                                                     \
+    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
     g.u = u; g.f = f; g.pid = pid; g.ktab = ktab; g.ntab = ntab; g.part = ws;                                \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \

@@ -35,11 +35,13 @@ _SIGS = {
     "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
     "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, LL, I, LL, P],
     "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, LL, P],
+    "mg_coarse_tail": [P, P, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
 }
 _EXTRA = {
     "fea_abi_version": ([], I),
     "fea_mg_layout": ([I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
     "fea_norm_workspace_bytes": ([I, I], ctypes.c_size_t),
+    "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I], ctypes.c_size_t),
 }
 
 _lib = None
@@ -94,6 +96,13 @@ def mg_layout(N, elem_size):
     if lib().fea_mg_layout(N, elem_size, ctypes.byref(ld), ctypes.byref(bs)) != 0:
         raise ValueError(f"feanet_amd: unsupported level size N={N} (need N = 2^k + 1 >= 5)")
     return ld.value, bs.value
+
+
+TAIL_LDS_LIMIT = 160 * 1024 - 1024
+
+
+def coarse_tail_lds_bytes(Nt, nlev, elem_size, multi):
+    return int(lib().fea_mg_coarse_tail_lds_bytes(Nt, nlev, elem_size, int(bool(multi))))
 
 
 def norm_workspace_bytes(B, N):

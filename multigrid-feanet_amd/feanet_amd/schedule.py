@@ -11,6 +11,8 @@ Steps:
                                        fused first (v = omd*f_l written to vout, then restricted)
   ("prolong_sweep", l, src, csrc, dst) dst = J_l(src + w1 P(v_{l+1}[csrc]), f_l)
   ("prolong_add", l, src, csrc, dst)   dst = src + w1 P(v_{l+1}[csrc])
+  ("coarse_tail", t, dst)              levels t..L-1 in one launch (coarse_tail.hip): from f_t and a
+                                       zero guess, the coarse part of this same schedule; v_t -> dst
 
 Semantics reproduced:
   * nu1 = nu2 = 1: MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372) == MultiGrid.iterate
@@ -25,7 +27,10 @@ def _other(b):
     return "b" if b == "a" else "a"
 
 
-def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a"):
+def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None):
+    """tail_from = t (1 <= t <= L-1): levels t..L-1 run as one coarse_tail step."""
+    if tail_from is not None and not (1 <= tail_from <= L - 1):
+        raise ValueError("vcycle_schedule: tail_from must be in [1, L-1]")
     if L < 1 or nu1 < 0 or nu2 < 0:
         raise ValueError("vcycle_schedule: need L >= 1, nu1, nu2 >= 0")
     if compat not in (None, "mm_interface_q2"):
@@ -51,7 +56,8 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a"):
     if q2:
         for _ in range((L - 1) * nu1):
             sweep(0)
-    for l in range(1, L - 1):
+    last_down = L - 1 if tail_from is None else tail_from
+    for l in range(1, last_down):
         if q2 or nu1 == 0:
             cur[l] = "zero"
             steps.append(("resid_restrict", l, "zero", None))
@@ -63,16 +69,22 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a"):
             for _ in range(nu1 - 1):
                 sweep(l)
             steps.append(("resid_restrict", l, cur[l], None))
-    # ---- coarsest
-    ncs = nu2 if q2 else nu1 + nu2
-    if ncs > 0:
-        sweep(L - 1, zero=True)
-        for _ in range(ncs - 1):
-            sweep(L - 1)
+    if tail_from is not None:
+        steps.append(("coarse_tail", tail_from, "a"))
+        cur[tail_from] = "a"
+        top = tail_from - 1
     else:
-        cur[L - 1] = "zero"
+        # ---- coarsest
+        ncs = nu2 if q2 else nu1 + nu2
+        if ncs > 0:
+            sweep(L - 1, zero=True)
+            for _ in range(ncs - 1):
+                sweep(L - 1)
+        else:
+            cur[L - 1] = "zero"
+        top = L - 2
     # ---- up
-    for l in range(L - 2, -1, -1):
+    for l in range(top, -1, -1):
         dst = "a" if cur[l] == "zero" else _other(cur[l])
         steps.append(("prolong_sweep" if nu2 >= 1 else "prolong_add", l, cur[l], cur[l + 1], dst))
         cur[l] = dst

@@ -77,11 +77,13 @@ class MultigridSolver:
         compat: None, or "mm_interface_q2" to reproduce MM_Interface_error.ipynb:141 (pre-smoothing
             applied to the finest grid at every depth).
         graph: replay the V-cycle as a HIP graph (default True).
+        coarse_tail: run every level with N <= 65 (below the finest) as one LDS-resident launch
+            (fea_mg_coarse_tail); False keeps one launch per level op.
     """
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
-                 nu1=1, nu2=1, compat=None, graph=True):
+                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True):
         if n < 2 or (n & (n - 1)) != 0:
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
         if dtype not in (torch.float32, torch.float64):
@@ -130,6 +132,20 @@ class MultigridSolver:
             pid = ms.interface_pattern_map(nl + 1, shape, size) if multi else None
             self.levels.append(_Level(nl, self.B, dtype, dev, pid))
         self.fine_pid = (torch.from_numpy(ms.interface_pattern_map(n + 1, shape, size)).to(dev) if multi else None)
+        self.tail_from = None
+        if coarse_tail:
+            esz = 4 if dtype == torch.float32 else 8
+            for l in range(1, self.L):
+                Nl = self.levels[l].N
+                if Nl <= 65 and _lib.coarse_tail_lds_bytes(Nl, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT:
+                    self.tail_from = l
+                    break
+        if self.tail_from is not None and multi:
+            maps = [ms.interface_pattern_map(self.levels[l].N, shape, size).reshape(-1)
+                    for l in range(self.tail_from, self.L)]
+            self.tail_pid = torch.from_numpy(np.concatenate(maps)).to(dev)
+        else:
+            self.tail_pid = None
         self.ws = torch.zeros(max(1, _lib.norm_workspace_bytes(self.B, n + 1) // 8), dtype=torch.float64,
                               device=dev)
         self.norm_out = torch.zeros(self.B, dtype=torch.float64, device=dev)
@@ -230,7 +246,7 @@ class MultigridSolver:
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
         lv = self.levels
-        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start)
+        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from)
         kt, om, nt = self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab
         rt, pt = self.rtab.data_ptr(), self.ptab.data_ptr()
         nr, npt = self.rtab.shape[0], self.ptab.shape[0]
@@ -262,6 +278,12 @@ class MultigridSolver:
             elif kind == "prolong_add":
                 plan.append(("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
                                                 self.w[1]) + geom(l) + cgeom(l)))
+            elif kind == "coarse_tail":
+                t = l
+                plan.append(("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].N, self.L - t, lv[t].ld,
+                                                lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
+                                                kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
+                                                int(self.compat == "mm_interface_q2"), lv[t].B)))
             else:  # pragma: no cover
                 raise AssertionError(kind)
         return plan, end

@@ -164,10 +164,11 @@ def test_mg_transfer(T, problem, learned, n, B):
 
 
 # ----------------------------------------------------------------------------- V-cycles
+@pytest.mark.parametrize("tail", [True, False])
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
-@pytest.mark.parametrize("n,L", [(64, None), (128, 4), (32, 1), (32, 2)])
-def test_vcycle_vs_oracle(T, problem, n, L):
+@pytest.mark.parametrize("n,L", [(64, None), (128, 4), (32, 1), (32, 2), (256, None)])
+def test_vcycle_vs_oracle(T, problem, n, L, tail):
     from feanet_amd.solver import MultigridSolver
     rng = np.random.default_rng(n)
     B = 2
@@ -178,18 +179,27 @@ def test_vcycle_vs_oracle(T, problem, n, L):
     mg_o.set_boundary(geo, bc)
     u0 = rng.standard_normal((B, N, N)).astype(npdt(T))
     f = rng.standard_normal((B, N, N)).astype(npdt(T))
-    s = MultigridSolver(n, levels=L, problem=problem, dtype=T, batch=B)
+    s = MultigridSolver(n, levels=L, problem=problem, dtype=T, batch=B, coarse_tail=tail)
+    if tail and s.L > 1 and n <= 256:
+        assert s.tail_from is not None
     s.set_boundary(torch.from_numpy(bc).cuda().reshape(B, 1, N, N))
     s.set_rhs(f=torch.from_numpy(f).cuda().reshape(B, 1, N, N))
     s.load(torch.from_numpy(u0).cuda().reshape(B, 1, N, N))
     v = u0 * geo + bc
+    r0 = orc.interior_norm(f - mg_o.levels[0].K(v))
     for k in range(4):
         s.vcycle()
         v = mg_o.step(v, f)
         got = s.solution().cpu().numpy()[:, 0]
-        scale = 1e-10 if T == torch.float64 else 2e-5
-        err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
-        assert err < scale, f"cycle {k}: {err:.3e}"
+        if T == torch.float64 or k == 0:
+            # fp64: every cycle; fp32: the first cycle (later iterates differ by cond(K)*eps32 ~ 1e-4
+            # between any two fp32 implementations, so fp32 is compared through the residual below)
+            err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
+            assert err < (1e-10 if T == torch.float64 else 2e-5), f"cycle {k}: {err:.3e}"
+        res = s.residual_norm().cpu().numpy()
+        ref = orc.interior_norm(f - mg_o.levels[0].K(v))
+        tol = 1e-9 if T == torch.float64 else 2e-3
+        np.testing.assert_allclose(res, ref, rtol=tol, atol=(1e-12 if T == torch.float64 else 1e-6) * r0.max())
 
 
 def test_vcycle_graph_replay_matches_eager():
@@ -269,7 +279,7 @@ def test_multigrid_py_learned_golden(gold):
         u, hist = s.solve(f=torch.from_numpy(g["f"]).cuda(), eps=5e-5, max_cycles=40)
         hist = np.array([h[0] for h in hist])
         assert len(hist) - 1 == ncyc == len(g[f"{tag}_hist"]) - 1
-        np.testing.assert_allclose(hist[:8], g[f"{tag}_hist"][:8], rtol=1e-3, atol=1e-6 * hist[0])
+        np.testing.assert_allclose(hist[:8], g[f"{tag}_hist"][:8], rtol=3e-3, atol=1e-5 * hist[0])
 
 
 def test_mm_convergence_golden(gold):
@@ -354,3 +364,33 @@ def test_batch_independence():
         s1.load()
         s1.vcycle(3)
         assert torch.equal(s1.solution()[0], ub[b])
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("Nt,nlev", [(5, 2), (9, 3), (17, 3), (33, 5), (65, 6), (65, 2)])
+@pytest.mark.parametrize("B", [1, 2])
+@pytest.mark.parametrize("nu", [(1, 1), (2, 1), (0, 2), (1, 0)])
+def test_coarse_tail_kernel(T, problem, Nt, nlev, B, nu):
+    """fea_mg_coarse_tail against the restatement of its sub-cycle with oracle operators."""
+    from feanet_amd import _lib, mesh_setup as ms
+    from test_schedule import tail_oracle
+    n = (Nt - 1) << 1  # a parent level above the tail (unused, only to build the hierarchy)
+    L = nlev + 1
+    mg = orc.OracleMultigrid(n, problem, npdt(T), levels=L)
+    rng = np.random.default_rng(Nt + nlev + B)
+    f = rng.standard_normal((B, Nt, Nt)).astype(npdt(T))
+    f[:, 0, :] = f[:, -1, :] = f[:, :, 0] = f[:, :, -1] = 0
+    ref = tail_oracle(mg, 1, f, None, B, nu1=nu[0], nu2=nu[1], q2=False)
+    fr = Frame(Nt - 1, B, T, problem)
+    fr.put("f", f)
+    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T)
+    pidl = None
+    if problem == "interface":
+        maps = [ms.interface_pattern_map(((Nt - 1) >> k) + 1).reshape(-1) for k in range(nlev)]
+        pidl = torch.from_numpy(np.concatenate(maps)).cuda()
+    _lib.call("mg_coarse_tail", T, fr.L.f.data_ptr(), fr.L.a.data_ptr(), Nt, nlev, fr.L.ld, fr.L.bs,
+              None if pidl is None else pidl.data_ptr(), kt.data_ptr(), om.data_ptr(), ktab.shape[0], rt.data_ptr(),
+              pt.data_ptr(), 1.0, 1.0, nu[0], nu[1], 0, B, None)
+    got = fr.get("a")
+    close(got, ref, T, f"tail Nt={Nt} nlev={nlev} B={B} nu={nu}")

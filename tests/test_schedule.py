@@ -40,6 +40,8 @@ def interpret(mg, steps, v, f, compat=None):
                 fs[l + 1] = mg._mm_restrict(r)
             else:
                 fs[l + 1] = orc.restrict(r, lv[l].pid, mg.rtab, mg.w[0])
+        elif kind == "coarse_tail":
+            bufs[l][st[2]] = tail_oracle(mg, l, fs[l], compat, B)
         elif kind in ("prolong_sweep", "prolong_add"):
             src = get(l, st[2])
             e = get(l + 1, st[3])
@@ -50,6 +52,55 @@ def interpret(mg, steps, v, f, compat=None):
             x = src + corr
             bufs[l][st[4]] = lv[l].sweep(x, fs[l]) if kind == "prolong_sweep" else x
     return bufs
+
+
+def tail_oracle(mg, t, f_t, compat, B, nu1=None, nu2=None, q2=None):
+    """The coarse_tail kernel's loop (coarse_tail.hip) restated with oracle ops."""
+    nu1 = mg.nu[0] if nu1 is None else nu1
+    nu2 = mg.nu[1] if nu2 is None else nu2
+    q2 = mg.q2 if q2 is None else q2
+    lv = mg.levels[t:]
+    dt = mg.dtype
+    zeros = lambda k: np.zeros((B, lv[k].N, lv[k].N), dt)
+    f = [f_t] + [None] * (len(lv) - 1)
+    v = [zeros(k) for k in range(len(lv))]
+    for k in range(len(lv) - 1):
+        if nu1 > 0 and not q2:
+            v[k] = lv[k].sweep(zeros(k), f[k])
+            for _ in range(nu1 - 1):
+                v[k] = lv[k].sweep(v[k], f[k])
+        r = f[k] - lv[k].K(v[k])
+        f[k + 1] = mg._mm_restrict(r) if compat == "mm" else orc.restrict(r, lv[k].pid, mg.rtab, mg.w[0])
+    k = len(lv) - 1
+    ncs = nu2 if q2 else nu1 + nu2
+    for s in range(ncs):
+        v[k] = lv[k].sweep(v[k], f[k])
+    for k in range(len(lv) - 2, -1, -1):
+        corr = (orc.bilinear_upsample(v[k + 1]) * lv[k].geo if compat == "mm"
+                else orc.prolong(v[k + 1], lv[k + 1].pid, mg.ptab, mg.w[1]))
+        v[k] = v[k] + corr
+        for _ in range(nu2):
+            v[k] = lv[k].sweep(v[k], f[k])
+    return v[0]
+
+
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("tail", [None, 1, 2, 4])
+def test_tail_schedule_equals_full(problem, tail):
+    n = 32
+    L = 5
+    rng = np.random.default_rng(11)
+    for nu, q2 in (((1, 1), False), ((2, 1), False), ((0, 2), False), ((1, 1), True)):
+        mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+        mg.nu, mg.q2 = nu, q2
+        v = rng.standard_normal((2, n + 1, n + 1))
+        f = rng.standard_normal((2, n + 1, n + 1))
+        compat = "mm_interface_q2" if q2 else None
+        ref_steps, ref_end = vcycle_schedule(L, *nu, compat=compat)
+        ref = interpret(mg, ref_steps, v, f)[0][ref_end]
+        steps, end = vcycle_schedule(L, *nu, compat=compat, tail_from=tail)
+        out = interpret(mg, steps, v, f)[0][end]
+        np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
 
 
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
