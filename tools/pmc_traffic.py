@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from two separate rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
+reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read -> doubled here;
+WRITE_SIZE is exact for 16 B/lane streaming stores.  Every load/store of the framed kernels is
+16 B/lane (halo loads included).
+
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [SUMMARY_TXT]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        per[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+    return per
+
+
+def short(n):
+    return n.replace("void ", "").replace("fea::", "").split("(")[0]
+
+
+def main(fcsv, wcsv, out_json, summary=None):
+    fetch = load(fcsv, "FETCH_SIZE")
+    write = load(wcsv, "WRITE_SIZE")
+    rows = []
+    for key in sorted(set(fetch) & set(write), key=lambda k: -sum(fetch[k])):
+        name, grid = key
+        f = 2 * 1024 * sum(fetch[key]) / len(fetch[key])
+        w = 1024 * sum(write[key]) / len(write[key])
+        rows.append((short(name), grid, len(fetch[key]), f, w))
+    res = {}
+    for name, grid, n, f, w in rows:
+        if name == "k_mg_sweep<double, false, false>" and grid == 262144:
+            nodes = 4095 * 4095
+            res["mg_sweep_f64_4097"] = {
+                "hbm_bytes_per_launch": f + w, "read_bytes_per_launch": f, "write_bytes_per_launch": w,
+                "algorithmic_bytes_per_launch": 24 * nodes, "launches": n,
+                "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads), KiB -> bytes",
+                "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (profiles/r01_pmc)"}
+    json.dump(res, open(out_json, "w"), indent=1)
+    if summary:
+        with open(summary, "w") as fh:
+            fh.write(f"{'kernel':45s} {'grid':>8s} {'n':>4s} {'read MB':>9s} {'write MB':>9s}\n")
+            for name, grid, n, f, w in rows:
+                fh.write(f"{name:45s} {grid:8d} {n:4d} {f / 1e6:9.2f} {w / 1e6:9.2f}\n")
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
