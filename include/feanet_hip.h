@@ -159,6 +159,18 @@ int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out
                                  const double* rtab, int nrtab, double w0, int B, int N, int ld,
                                  long long bstride, int ldc, long long bstridec, void* stream);
 
+/* Fused pre-smooth + residual + restriction on a level with a given iterate (temporal blocking):
+ *   u_out = J(u, f) (interior)   and   fc(interior) = w0 * R(f - K u_out)
+ * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357). */
+int fea_mg_sweep_restrict_f32(const float* u, const float* f, float* u_out, float* fc, const uint8_t* pid,
+                              const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
+                              float w0, int B, int N, int ld, long long bstride, int ldc, long long bstridec,
+                              void* stream);
+int fea_mg_sweep_restrict_f64(const double* u, const double* f, double* u_out, double* fc, const uint8_t* pid,
+                              const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
+                              double w0, int B, int N, int ld, long long bstride, int ldc, long long bstridec,
+                              void* stream);
+
 /* Fused prolongation + correction + post-sweep:
  *   out = J(u + w1 * P(ec), f)   (P kernel by coarse-node pattern pidc)
  * FEANet/multigrid.py:177-181 (Interpolate, add, Relax) in one pass. */

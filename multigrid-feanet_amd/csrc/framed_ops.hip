@@ -18,6 +18,8 @@
 //     order so row-adjacent tasks share an L2.
 // Roofline: these kernels are HBM-bound (~0.9 flop/byte in fp64); algorithmic bytes per fine node
 // are documented in DESIGN.md (sweep 24 B, residual+restrict 18 B, prolong+sweep 26 B in fp64).
+#include <cstdlib>
+
 #include "fea_common.h"
 
 namespace fea {
@@ -126,7 +128,10 @@ template <typename T, int V>
 __device__ __forceinline__ RawRow<T, V> raw_row(const T* __restrict__ rp, int lane) {
   RawRow<T, V> r;
   vload<T, V>(rp + V * lane, r.x);
-  vload<T, V>(rp + (lane < 32 ? -V : kWave * V), r.h);
+  // halo: only the two edge lanes load (exec-masked), the other lanes' h is never read
+#pragma unroll
+  for (int k = 0; k < V; ++k) r.h[k] = T(0);
+  if (lane == 0 || lane == kWave - 1) vload<T, V>(rp + (lane == 0 ? -V : kWave * V), r.h);
   return r;
 }
 
@@ -145,7 +150,9 @@ template <int V>
 __device__ __forceinline__ RawP<V> raw_prow(const uint8_t* __restrict__ pp, int lane) {
   RawP<V> r;
   pload<V>(pp + V * lane, r.x);
-  pload<V>(pp + (lane < 32 ? -V : kWave * V), r.h);
+#pragma unroll
+  for (int k = 0; k < V; ++k) r.h[k] = 0;
+  if (lane == 0 || lane == kWave - 1) pload<V>(pp + (lane == 0 ? -V : kWave * V), r.h);
   return r;
 }
 
@@ -522,6 +529,327 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel E: fused pre-smooth + residual + restriction on a level with a given iterate
+// (temporal blocking of FEANet/multigrid.py:165 then :168-170):
+//   u' = J(u, f)  (stored, interior)     f_c = w0 R(f - K u')
+// One pass reads u and f once (plus halos) instead of twice.  The residual of a row needs u' at
+// the lane's window columns L..RR; inner lanes get them from neighbours by DPP, the two edge lanes
+// compute u' at their halo columns themselves (lane 0: c0-1; lane 63: c0+SW, c0+SW+1).
+// ---------------------------------------------------------------------------
+template <typename T, int V>
+struct XRaw {  // row load with the extra halo column(s) the edge sweeps need
+  T x[V], h[V], hx;
+};
+template <int V>
+struct XRawP {
+  int x[V], h[V], hx;
+};
+template <typename T, int V>
+struct XRow {
+  Row<T, V> w;
+  T el, er;  // lane 0: column c0-2; lane 63: column c0+SW+2 (other lanes: unused)
+};
+template <int V>
+struct XPRow {
+  PRow<V> w;
+  int el, er;
+};
+
+template <typename T, int V>
+__device__ __forceinline__ XRaw<T, V> xraw_row(const T* __restrict__ rp, int lane) {
+  XRaw<T, V> r;
+  vload<T, V>(rp + V * lane, r.x);
+#pragma unroll
+  for (int k = 0; k < V; ++k) r.h[k] = T(0);
+  r.hx = T(0);
+  if (lane == 0 || lane == kWave - 1) {
+    vload<T, V>(rp + (lane == 0 ? -V : kWave * V), r.h);
+    if constexpr (V == 2) {
+      if (lane == kWave - 1) r.hx = rp[kWave * V + 2];
+    }
+  }
+  return r;
+}
+template <int V>
+__device__ __forceinline__ XRawP<V> xraw_prow(const uint8_t* __restrict__ pp, int lane) {
+  XRawP<V> r;
+  pload<V>(pp + V * lane, r.x);
+#pragma unroll
+  for (int k = 0; k < V; ++k) r.h[k] = 0;
+  r.hx = 0;
+  if (lane == 0 || lane == kWave - 1) {
+    pload<V>(pp + (lane == 0 ? -V : kWave * V), r.h);
+    if constexpr (V == 2) {
+      if (lane == kWave - 1) r.hx = pp[kWave * V + 2];
+    }
+  }
+  return r;
+}
+template <typename T, int V>
+__device__ __forceinline__ XRow<T, V> xfinish(const XRaw<T, V>& r) {
+  XRow<T, V> o;
+  RawRow<T, V> rr;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    rr.x[k] = r.x[k];
+    rr.h[k] = r.h[k];
+  }
+  o.w = finish(rr);
+  o.el = r.h[V - 2];                       // lane 0: c0-2
+  o.er = (V == 2) ? r.hx : r.h[2 % V];     // lane 63: c0+SW+2
+  return o;
+}
+template <int V>
+__device__ __forceinline__ XPRow<V> xfinish(const XRawP<V>& r) {
+  XPRow<V> o;
+  RawP<V> rr;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    rr.x[k] = r.x[k];
+    rr.h[k] = r.h[k];
+  }
+  o.w = finish(rr);
+  o.el = r.h[V - 2] * kTabStride;
+  o.er = ((V == 2) ? r.hx : r.h[2 % V]) * kTabStride;
+  return o;
+}
+
+#ifndef FEA_SR_WAVES_PER_EU
+#define FEA_SR_WAVES_PER_EU 1  // forcing 3 (168 VGPRs) spills and measured slower (119 vs 107 us)
+#endif
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 : FEA_SR_WAVES_PER_EU))) void k_mg_sweep_restrict(MgArgs<T> g) {
+  using F = Frame<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int N = g.N, Nc = g.Nc;
+  const int c0 = 1 + id.s * F::SW;
+  const int I0 = 1 + id.t * (g.rb / 2);
+  const int I1 = min(I0 + g.rb / 2, Nc - 1);
+  const int cl = c0 + V * lane;
+  T ks[9], rs[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      rs[d] = g.rtab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w0 = g.w;
+  const bool L0 = lane == 0, L63 = lane == kWave - 1;
+  // interior flags of the window columns: j = 0..V+2 (L, own, R, RR) and the edge-sweep centres
+  bool cin[V + 3];
+#pragma unroll
+  for (int j = 0; j < V + 3; ++j) {
+    const int c = cl + j - 1;
+    cin[j] = c >= 1 && c <= N - 2;
+  }
+  const int ce1 = L0 ? c0 - 1 : c0 + F::SW;  // centre column of edge sweep 1
+  const bool e1in = ce1 >= 1 && ce1 <= N - 2;
+  const bool e2in = c0 + F::SW + 1 <= N - 2;  // edge sweep 2 (lane 63): column c0+SW+1
+  const long long poff = F::OFF + c0;
+  const long long boff = (long long)id.b * g.bs + poff;
+  const T* __restrict__ ub = g.u + boff;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ ob = g.out2 + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
+  const int ld = g.ld;
+  const int bc0 = (c0 + 1) / 2;
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
+  const int Jl = bc0 + Q * lane;
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), N) + 1) * ld; };
+
+  struct RawS {
+    XRaw<T, V> u;
+    RawRow<T, V> f;
+    XRawP<V> p;
+  };
+  struct S {  // one row of the input window
+    XRow<T, V> u;
+    Row<T, V> f;
+    XPRow<V> p;
+  };
+  auto raw_s = [&](int y) {
+    RawS r;
+    r.u = xraw_row<T, V>(ub + rowo(y), lane);
+    r.f = raw_row<T, V>(fb + rowo(y), lane);
+    if constexpr (MULTI) r.p = xraw_prow<V>(pb + rowo(y), lane);
+    return r;
+  };
+  auto fin_s = [&](const RawS& r) {
+    S s_;
+    s_.u = xfinish(r.u);
+    s_.f = finish(r.f);
+    if constexpr (MULTI) s_.p = xfinish(r.p);
+    return s_;
+  };
+  // weight of tap d at a node with table offset o
+  auto kw = [&](int o, int d) -> T { return MULTI ? tab[o + d] : ks[d]; };
+  // u' row y (window columns L..RR) from input rows y-1, y, y+1 (a, b, c); boundary rows/cols keep u
+  auto usweep = [&](const S& a, const S& b, const S& c, int y) {
+    Row<T, V> o;
+    const bool rin = y >= 1 && y <= N - 2;
+    T own[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T acc = kapply<T, V, MULTI>(a.u.w, b.u.w, c.u.w, a.p.w, b.p.w, c.p.w, k, ks, tab);
+      const T omk = MULTI ? tab[b.p.w.a[k + 1] + 9] : om;
+      const T v = omk * (b.f.a[k + 1] - acc) + b.u.w.a[k + 1];
+      own[k] = (rin && cin[k + 1]) ? v : b.u.w.a[k + 1];
+    }
+    // edge sweep 1: lane 0 at c0-1 (cols c0-2, c0-1, c0); lane 63 at c0+SW (cols c0+SW-1, +SW, +SW+1)
+    T e1, e2;
+    {
+      const S* rows[3] = {&a, &b, &c};
+      T acc = 0;
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const S& q = *rows[dr];
+        const T vm = L0 ? q.u.el : q.u.w.a[V];
+        const T vc = L0 ? q.u.w.a[0] : q.u.w.a[V + 1];
+        const T vp = L0 ? q.u.w.a[1] : q.u.w.a[V + 2];
+        int om_ = 0, oc = 0, op = 0;
+        if constexpr (MULTI) {
+          om_ = L0 ? q.p.el : q.p.w.a[V];
+          oc = L0 ? q.p.w.a[0] : q.p.w.a[V + 1];
+          op = L0 ? q.p.w.a[1] : q.p.w.a[V + 2];
+        }
+        acc += kw(om_, dr * 3 + 0) * vm;
+        acc += kw(oc, dr * 3 + 1) * vc;
+        acc += kw(op, dr * 3 + 2) * vp;
+      }
+      const T uc = L0 ? b.u.w.a[0] : b.u.w.a[V + 1];
+      const T fc = L0 ? b.f.a[0] : b.f.a[V + 1];
+      const T omc = MULTI ? tab[(L0 ? b.p.w.a[0] : b.p.w.a[V + 1]) + 9] : om;
+      const T v = omc * (fc - acc) + uc;
+      e1 = (rin && e1in) ? v : uc;
+    }
+    {  // edge sweep 2 (meaningful in lane 63): centre c0+SW+1, cols c0+SW .. c0+SW+2
+      const S* rows[3] = {&a, &b, &c};
+      T acc = 0;
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const S& q = *rows[dr];
+        int om_ = 0, oc = 0, op = 0;
+        if constexpr (MULTI) {
+          om_ = q.p.w.a[V + 1];
+          oc = q.p.w.a[V + 2];
+          op = q.p.er;
+        }
+        acc += kw(om_, dr * 3 + 0) * q.u.w.a[V + 1];
+        acc += kw(oc, dr * 3 + 1) * q.u.w.a[V + 2];
+        acc += kw(op, dr * 3 + 2) * q.u.er;
+      }
+      const T uc = b.u.w.a[V + 2];
+      const T omc = MULTI ? tab[b.p.w.a[V + 2] + 9] : om;
+      const T v = omc * (b.f.a[V + 2] - acc) + uc;
+      e2 = (rin && e2in) ? v : uc;
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) o.a[k + 1] = own[k];
+    o.a[0] = shr1(own[V - 1], e1);
+    o.a[V + 1] = shl1(own[0], e1);
+    o.a[V + 2] = shl1(own[1 % V], e2);
+    return o;
+  };
+  auto store_u = [&](int y, const Row<T, V>& w) {
+    const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Nc - 1) && y <= N - 2;
+    if (own) {
+      T o[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = w.a[k + 1];
+      store_masked<T, V>(ob + rowo(y) + V * lane, o, cl, N);
+    }
+  };
+  const int ya = 2 * I0 - 1;  // first residual row
+  auto resid_p = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const S& pa, const S& pb_,
+                     const S& pc, const S& sy, T (&r)[V + 1]) {
+#pragma unroll
+    for (int k = 0; k <= V; ++k)
+      r[k] = sy.f.a[k + 1] - kapply<T, V, MULTI>(a, b, c, pa.p.w, pb_.p.w, pc.p.w, k, ks, tab);
+  };
+  // restriction accumulated row by row: a fine residual row with kernel row ky contributes
+  // R[ky][kx] * r[2q + kx] to coarse output q (per fine-node pattern in the MULTI case)
+  auto racc = [&](T (&acc)[Q], const T (&r)[V + 1], const PRow<V>& p, int ky, bool init) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      T t;
+      if constexpr (!MULTI) {
+        t = rs[ky * 3 + 0] * r[2 * q];
+        t += rs[ky * 3 + 1] * r[2 * q + 1];
+        t += rs[ky * 3 + 2] * r[2 * q + 2];
+      } else {
+        t = rtb[p.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
+        t += rtb[p.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
+        t += rtb[p.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
+      }
+      acc[q] = init ? t : acc[q] + t;
+    }
+  };
+  // input rows ya-2 .. ya+2 first
+  S X0 = fin_s(raw_s(ya - 2)), X1 = fin_s(raw_s(ya - 1)), X2 = fin_s(raw_s(ya)), X3 = fin_s(raw_s(ya + 1));
+  RawS nB = raw_s(ya + 3);  // row 2I0+2, consumed in the first half of the first iteration
+  S X4 = fin_s(raw_s(ya + 2));
+  Row<T, V> Uc = usweep(X1, X2, X3, ya);  // u'(2I0-1)
+  store_u(ya, Uc);
+  Row<T, V> Un = usweep(X2, X3, X4, ya + 1);  // u'(2I0)
+  store_u(ya + 1, Un);
+  T acc[Q];
+  {
+    const Row<T, V> Up = usweep(X0, X1, X2, ya - 1);  // u'(2I0-2)
+    T r[V + 1];
+    resid_p(Up, Uc, Un, X1, X2, X3, X2, r);  // residual row 2I0-1 -> coarse I0 with ky = 0
+    racc(acc, r, X2.p.w, 0, true);
+  }
+  // loop state for coarse row I: acc holds the ky = 0 part (fine row 2I-1); u' rows 2I-1 (Uc), 2I (Un);
+  // input rows 2I-1 (X2), 2I (X3), 2I+1 (X4); raw row 2I+2 (nB) in flight.
+  for (int I = I0; I < I1; ++I) {
+    const RawS m1 = raw_s(2 * I + 3);  // consumed in the second half of this iteration
+    const S X5 = fin_s(nB);            // row 2I+2
+    const Row<T, V> U1 = usweep(X3, X4, X5, 2 * I + 1);
+    store_u(2 * I + 1, U1);
+    T r[V + 1];
+    resid_p(Uc, Un, U1, X2, X3, X4, X3, r);  // residual row 2I
+    racc(acc, r, X3.p.w, 1, false);
+    const RawS m2 = raw_s(2 * I + 4);  // consumed in the first half of the next iteration
+    const S X6 = fin_s(m1);            // row 2I+3
+    const Row<T, V> U2 = usweep(X4, X5, X6, 2 * I + 2);
+    store_u(2 * I + 2, U2);
+    resid_p(Un, U1, U2, X3, X4, X5, X4, r);  // residual row 2I+1: ky = 2 for I, ky = 0 for I+1
+    racc(acc, r, X4.p.w, 2, false);
+    T o[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) o[q] = w0 * acc[q];
+    racc(acc, r, X4.p.w, 0, true);
+    T* cp = cb + (long long)(I + 1) * g.ldc;
+    if (Jl + Q - 1 <= Nc - 2) {
+      vstore<T, Q>(cp, o);
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (Jl + q <= Nc - 2) cp[q] = o[q];
+    }
+    Uc = U1;
+    Un = U2;
+    X2 = X4;
+    X3 = X5;
+    X4 = X6;
+    nB = m2;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Kernel C: fused prolongation + correction (+ post-sweep):
 //   v = u + w1 * P(ec)   (P kernel of the coarse node);   out = SWEEP ? J(v, f) : v
 // ---------------------------------------------------------------------------
@@ -837,10 +1165,17 @@ static inline bool mg_n_ok(int N) {
 
 // Rows per wave task: the largest even count (<= kRB) that still gives >= kTargetWaves waves,
 // so small levels are spread over the chip instead of being marched row by row by a few waves.
-constexpr int kTargetWaves = 4096;
+static int target_waves() {
+  static const int tw = [] {
+    const char* e = getenv("FEANET_TARGET_WAVES");  // tuning knob (default 2048 = 8 waves per CU)
+    return e ? std::max(64, atoi(e)) : 2048;
+  }();
+  return tw;
+}
 static inline int pick_rb(int B, int nstrips, int rows) {
+  const int tw = target_waves();
   for (int rb = kRB; rb > 2; rb /= 2)
-    if ((long long)B * nstrips * div_up(rows, rb) >= kTargetWaves) return rb;
+    if ((long long)B * nstrips * div_up(rows, rb) >= tw) return rb;
   return 2;
 }
 
@@ -946,6 +1281,27 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
       if (multi) k_mg_resid_restrict<T, true, false><<<grid, 256, 0, s>>>(g);                                \
       else k_mg_resid_restrict<T, false, false><<<grid, 256, 0, s>>>(g);                                     \
     }                                                                                                        \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_mg_sweep_restrict_##SUF(const T* u, const T* f, T* u_out, T* fc, const uint8_t* pid,       \
+                                             const T* ktab, const T* omd, int ntab, const T* rtab, int nrtab,    \
+                                             T w0, int B, int N, int ld, long long bs, int ldc, long long bsc,  \
+                                             void* stream) {                                                   \
+    if (!u || !f || !u_out || !fc || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(N, ld, bs) || u_out == u) \
+      return FEA_EINVAL;                                                                                     \
+    const int Nc = (N + 1) / 2;                                                                              \
+    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || (nrtab != ntab && nrtab != 1))          \
+      return FEA_EINVAL;                                                                                     \
+    if (ntab > 1 && nrtab == 1) return FEA_EINVAL;                                                           \
+    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                  \
+    g.u = u; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
+    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;                           \
+    g.ntr = div_up(Nc - 2, g.rb / 2);                                                                        \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (ntab > 1) k_mg_sweep_restrict<T, true><<<grid, 256, 0, s>>>(g);                                      \
+    else k_mg_sweep_restrict<T, false><<<grid, 256, 0, s>>>(g);                                              \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \

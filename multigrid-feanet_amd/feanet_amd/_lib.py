@@ -32,6 +32,7 @@ _SIGS = {
     "mg_unpack": [P, P, I, I, I, LL, P],
     "mg_sweep": [P, P, P, P, P, P, I, I, I, I, LL, P],
     "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
+    "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
     "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
     "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, LL, I, LL, P],
     "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, LL, P],
@@ -62,7 +63,7 @@ def lib():
     if not os.path.exists(LIB):
         raise RuntimeError(f"feanet_amd: {LIB} is missing; run `python -m feanet_amd.build` "
                            "(there is no CPU fallback for the HIP path)")
-    L = ctypes.CDLL(LIB)
+    L = ctypes.CDLL(os.environ.get("FEANET_LIB_OVERRIDE", LIB))  # override: A/B tuning builds only
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

@@ -34,7 +34,10 @@ def build(force=False, verbose=True):
     if not force and not needs_build():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -ffp-contract=on: a*b+c is fused only within one source expression, so a value recomputed
+    # at a different call site (task-edge rows, edge lanes) rounds identically -> results are
+    # independent of rows-per-task and batch size (bitwise)
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-ffp-contract=on", "-std=c++17", "-fPIC", "-shared",
            "-Wno-pass-failed", f"-I{INCLUDE}", f"-I{CSRC}", *sources(), "-o", LIB + ".tmp"]
     if verbose:
         print("[feanet_amd.build]", " ".join(cmd), file=sys.stderr)

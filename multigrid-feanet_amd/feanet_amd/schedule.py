@@ -9,6 +9,7 @@ Steps:
   ("sweep", l, src, dst)               dst = J_l(src, f_l); src None means a zero initial guess
   ("resid_restrict", l, src, vout)     f_{l+1} = w0 R(f_l - K_l src); src None: zero-guess sweep
                                        fused first (v = omd*f_l written to vout, then restricted)
+  ("sweep_restrict", l, src, dst)      dst = J_l(src, f_l) and f_{l+1} = w0 R(f_l - K_l dst) in one pass
   ("prolong_sweep", l, src, csrc, dst) dst = J_l(src + w1 P(v_{l+1}[csrc]), f_l)
   ("prolong_add", l, src, csrc, dst)   dst = src + w1 P(v_{l+1}[csrc])
   ("coarse_tail", t, dst)              levels t..L-1 in one launch (coarse_tail.hip): from f_t and a
@@ -27,8 +28,10 @@ def _other(b):
     return "b" if b == "a" else "a"
 
 
-def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None):
-    """tail_from = t (1 <= t <= L-1): levels t..L-1 run as one coarse_tail step."""
+def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fuse=True):
+    """tail_from = t (1 <= t <= L-1): levels t..L-1 run as one coarse_tail step.
+    fuse: the last pre-sweep of a level with a given iterate runs fused with its residual and
+    restriction (sweep_restrict)."""
     if tail_from is not None and not (1 <= tail_from <= L - 1):
         raise ValueError("vcycle_schedule: tail_from must be in [1, L-1]")
     if L < 1 or nu1 < 0 or nu2 < 0:
@@ -49,10 +52,29 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None):
             sweep(0)
         return steps, cur[0]
     q2 = compat == "mm_interface_q2"
+
+    def presmooth_restrict(l, nsweeps, from_zero):
+        """nsweeps pre-sweeps of level l (the first from zero if from_zero), then residual + restriction."""
+        if nsweeps == 0:
+            steps.append(("resid_restrict", l, cur[l], None))
+            return
+        if from_zero and nsweeps == 1:
+            steps.append(("resid_restrict", l, None, "a"))
+            cur[l] = "a"
+            return
+        first = True
+        for i in range(nsweeps - (1 if fuse else 0)):
+            sweep(l, zero=(from_zero and first))
+            first = False
+        if fuse:
+            dst = _other(cur[l]) if cur[l] != "zero" else "a"
+            steps.append(("sweep_restrict", l, cur[l], dst))
+            cur[l] = dst
+        else:
+            steps.append(("resid_restrict", l, cur[l], None))
+
     # ---- down
-    for _ in range(nu1):
-        sweep(0)
-    steps.append(("resid_restrict", 0, cur[0], None))
+    presmooth_restrict(0, nu1, False)
     if q2:
         for _ in range((L - 1) * nu1):
             sweep(0)
@@ -61,14 +83,8 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None):
         if q2 or nu1 == 0:
             cur[l] = "zero"
             steps.append(("resid_restrict", l, "zero", None))
-        elif nu1 == 1:
-            steps.append(("resid_restrict", l, None, "a"))
-            cur[l] = "a"
         else:
-            sweep(l, zero=True)
-            for _ in range(nu1 - 1):
-                sweep(l)
-            steps.append(("resid_restrict", l, cur[l], None))
+            presmooth_restrict(l, nu1, True)
     if tail_from is not None:
         steps.append(("coarse_tail", tail_from, "a"))
         cur[tail_from] = "a"

@@ -79,11 +79,13 @@ class MultigridSolver:
         graph: replay the V-cycle as a HIP graph (default True).
         coarse_tail: run every level with N <= 65 (below the finest) as one LDS-resident launch
             (fea_mg_coarse_tail); False keeps one launch per level op.
+        fuse: run the last pre-sweep of a level fused with its residual + restriction
+            (fea_mg_sweep_restrict, one read of u and f); False issues them separately.
     """
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
-                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True):
+                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True):
         if n < 2 or (n & (n - 1)) != 0:
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
         if dtype not in (torch.float32, torch.float64):
@@ -102,6 +104,7 @@ class MultigridSolver:
         self.nu1, self.nu2 = int(nu1), int(nu2)
         self.compat = compat
         self.use_graph = graph
+        self.fuse = fuse
         npdt = np.float32 if dtype == torch.float32 else np.float64
         multi = problem == "interface"
         if problem not in ("poisson", "interface"):
@@ -246,7 +249,7 @@ class MultigridSolver:
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
         lv = self.levels
-        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from)
+        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse)
         kt, om, nt = self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab
         rt, pt = self.rtab.data_ptr(), self.ptab.data_ptr()
         nr, npt = self.rtab.shape[0], self.ptab.shape[0]
@@ -272,6 +275,9 @@ class MultigridSolver:
             elif kind == "resid_restrict":
                 plan.append(("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
                                                       kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l)))
+            elif kind == "sweep_restrict":
+                plan.append(("mg_sweep_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
+                                                   kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l)))
             elif kind == "prolong_sweep":
                 plan.append(("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
                                                   pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l)))
@@ -349,7 +355,10 @@ class MultigridSolver:
         pb = 1 if self.problem == "interface" else 0
         total = 0
         for name, args in self._plan(self._state)[0]:
-            B, N = args[-6:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add") else args[-4:-2]
+            if name == "mg_coarse_tail":
+                continue
+            B, N = (args[-6:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",
+                                            "mg_sweep_restrict") else args[-4:-2])
             nodes = B * (N - 2) ** 2
             coarse = B * ((N + 1) // 2 - 2) ** 2
             if name == "mg_sweep":
@@ -358,6 +367,8 @@ class MultigridSolver:
                 total += nodes * (esz * (2 if args[0] is not None else 2) + pb) + coarse * esz
                 if args[0] is None:
                     total += nodes * esz  # v written
+            elif name == "mg_sweep_restrict":
+                total += nodes * (3 * esz + pb) + coarse * esz
             elif name == "mg_prolong_sweep":
                 total += nodes * (3 * esz + pb) + coarse * (esz + pb)
             elif name == "mg_prolong_add":

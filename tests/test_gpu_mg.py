@@ -136,6 +136,16 @@ def test_mg_transfer(T, problem, learned, n, B):
               kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, w0, *fr.args(), co.L.ld, co.L.bs, None)
     ref = orc.restrict(f - orc.knet_apply(u, fr.pid_np, ktab), fr.pid_np, R, w0)
     close(co.get("f"), ref, T, "residual+restrict")
+    # fused pre-sweep + residual + restriction: u' = J(u, f) stored, fc = R(f - K u')
+    fr.put("b", u * 0 + 7.0)
+    _lib.call("mg_sweep_restrict", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), co.L.f.data_ptr(),
+              fr.pid(), kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    geo, _ = orc.square_geometry(fr.N, npdt(T))
+    up = orc.jacobi_sweep(u, f, fr.pid_np, ktab, geo, u * (1 - geo))
+    outb = fr.get("b")
+    close(outb[:, 1:-1, 1:-1], up[:, 1:-1, 1:-1], T, "fused sweep u'")
+    assert (outb[:, 0, :] == 7).all() and (outb[:, :, 0] == 7).all() and (outb[:, :, -1] == 7).all()
+    close(co.get("f"), orc.restrict(f - orc.knet_apply(up, fr.pid_np, ktab), fr.pid_np, R, w0), T, "fused RR")
     # zero-guess sweep fused: v = omd*f written, restriction of f - K v
     fr.put("b", u * 0)
     _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), fr.L.b.data_ptr(), co.L.f.data_ptr(), fr.pid(),
@@ -164,11 +174,13 @@ def test_mg_transfer(T, problem, learned, n, B):
 
 
 # ----------------------------------------------------------------------------- V-cycles
-@pytest.mark.parametrize("tail", [True, False])
+@pytest.mark.parametrize("tail,fuse", [(True, True), (False, False), (True, False)])
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
-@pytest.mark.parametrize("n,L", [(64, None), (128, 4), (32, 1), (32, 2), (256, None)])
-def test_vcycle_vs_oracle(T, problem, n, L, tail):
+@pytest.mark.parametrize("n,L", [(64, None), (128, 4), (32, 1), (32, 2), (256, None), (1024, None)])
+def test_vcycle_vs_oracle(T, problem, n, L, tail, fuse):
+    if problem == "interface" and n > 256:
+        pytest.skip("oracle pattern search kept small")
     from feanet_amd.solver import MultigridSolver
     rng = np.random.default_rng(n)
     B = 2
@@ -179,7 +191,7 @@ def test_vcycle_vs_oracle(T, problem, n, L, tail):
     mg_o.set_boundary(geo, bc)
     u0 = rng.standard_normal((B, N, N)).astype(npdt(T))
     f = rng.standard_normal((B, N, N)).astype(npdt(T))
-    s = MultigridSolver(n, levels=L, problem=problem, dtype=T, batch=B, coarse_tail=tail)
+    s = MultigridSolver(n, levels=L, problem=problem, dtype=T, batch=B, coarse_tail=tail, fuse=fuse)
     if tail and s.L > 1 and n <= 256:
         assert s.tail_from is not None
     s.set_boundary(torch.from_numpy(bc).cuda().reshape(B, 1, N, N))
@@ -264,8 +276,9 @@ def test_mm_interface_golden(gold):
         s.vcycle()
         hist.append(float(s.residual_norm()[0]))
     assert len(hist) == 14
-    np.testing.assert_allclose(hist[:8], g["hist"][:8], rtol=1e-3)
-    np.testing.assert_allclose(hist[:6], rec["mm_interface_res"][:6], rtol=2e-3)
+    # fp32 histories of two implementations agree to ~1e-3 relative (rounding differs per op order)
+    np.testing.assert_allclose(hist[:8], g["hist"][:8], rtol=3e-3, atol=1e-5 * g["hist"][0])
+    np.testing.assert_allclose(hist[:6], rec["mm_interface_res"][:6], rtol=3e-3)
 
 
 def test_multigrid_py_learned_golden(gold):

@@ -40,6 +40,11 @@ def interpret(mg, steps, v, f, compat=None):
                 fs[l + 1] = mg._mm_restrict(r)
             else:
                 fs[l + 1] = orc.restrict(r, lv[l].pid, mg.rtab, mg.w[0])
+        elif kind == "sweep_restrict":
+            out = lv[l].sweep(get(l, st[2]), fs[l])
+            bufs[l][st[3]] = out
+            r = fs[l] - lv[l].K(out)
+            fs[l + 1] = mg._mm_restrict(r) if compat == "mm" else orc.restrict(r, lv[l].pid, mg.rtab, mg.w[0])
         elif kind == "coarse_tail":
             bufs[l][st[2]] = tail_oracle(mg, l, fs[l], compat, B)
         elif kind in ("prolong_sweep", "prolong_add"):
@@ -103,28 +108,30 @@ def test_tail_schedule_equals_full(problem, tail):
         np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
 
 
+@pytest.mark.parametrize("fuse", [True, False])
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
 @pytest.mark.parametrize("L", [1, 2, 3, 5])
-def test_step_schedule_equals_reference_step(problem, L):
+def test_step_schedule_equals_reference_step(problem, L, fuse):
     n = 32
     rng = np.random.default_rng(L)
     mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
     v = rng.standard_normal((2, n + 1, n + 1))
     f = rng.standard_normal((2, n + 1, n + 1))
-    steps, end = vcycle_schedule(L, 1, 1)
+    steps, end = vcycle_schedule(L, 1, 1, fuse=fuse)
     out = interpret(mg, steps, v, f)[0][end]
     ref = mg.step(v, f)
     np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
 
 
+@pytest.mark.parametrize("fuse", [True, False])
 @pytest.mark.parametrize("nu", [(1, 1), (0, 1), (1, 0), (2, 1), (1, 2), (2, 2), (0, 2), (2, 0), (3, 1)])
-def test_nu_schedules_equal_rec_vcycle(nu):
+def test_nu_schedules_equal_rec_vcycle(nu, fuse):
     n = 32
     rng = np.random.default_rng(sum(nu))
     mg = orc.OracleMultigrid(n, "poisson", np.float64)
     v = rng.standard_normal((1, n + 1, n + 1))
     f = rng.standard_normal((1, n + 1, n + 1))
-    steps, end = vcycle_schedule(mg.L, *nu)
+    steps, end = vcycle_schedule(mg.L, *nu, fuse=fuse)
     out = interpret(mg, steps, v, f, compat="mm")[0][end]
     ref = mg.rec_vcycle(v, f, *nu)
     np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
@@ -145,9 +152,13 @@ def test_q2_schedule_equals_mm_interface():
 def test_schedule_shape_and_buffers():
     steps, end = vcycle_schedule(12, 1, 1)
     kinds = [s[0] for s in steps]
-    # 1 fine sweep, 11 residual-restrictions, 2 coarsest sweeps, 11 fused prolong+sweep
+    # fine sweep fused with its residual-restriction, 10 zero-guess residual-restrictions,
+    # 2 coarsest sweeps, 11 fused prolong+sweep
+    assert kinds.count("sweep_restrict") == 1 and kinds.count("resid_restrict") == 10
+    assert kinds.count("sweep") == 2 and kinds.count("prolong_sweep") == 11 and end == "a"
+    steps, end = vcycle_schedule(12, 1, 1, fuse=False)
+    kinds = [s[0] for s in steps]
     assert kinds.count("sweep") == 3 and kinds.count("resid_restrict") == 11
-    assert kinds.count("prolong_sweep") == 11 and end == "a"
     for s in steps:  # no step reads and writes the same buffer
         if s[0] == "sweep":
             assert s[2] != s[3]
