@@ -6,10 +6,12 @@ fused HIP kernels on a 4097 x 4097 fp64 Poisson problem resident in HBM (synthet
 right-hand side, zero initial guess), replayed as a HIP graph.  value = B * N^2 * ranks / t_step.
 
 Also reported on the same JSON line:
-  roofline      the dominant kernel (fine-level Ke-stencil Jacobi sweep, fea_mg_sweep at 4097^2):
+  roofline      the north-star kernel (fine-level Ke-stencil Jacobi sweep, fea_mg_sweep at 4097^2):
                 algorithmic bytes per launch (24 B per interior node: read u, read f, write u')
                 / its average duration from HIP events on its stream, vs the 8 TB/s HBM peak;
-                `traffic` = measured HBM bytes per launch from rocprofv3 PMC (profiles/, if present)
+                `traffic` = measured HBM bytes per launch from rocprofv3 PMC (profiles/, if present);
+                fine_level_kernels: the same measurement for the two fused level-0 kernels the V-cycle
+                runs (sweep+residual+restriction, prolongation+correction+sweep)
   cpu_baseline  the CPU oracle (numpy restatement of the reference V-cycle, 1 thread) on the same
                 workload, a bounded sample of whole V-cycles, rank 0 at N = 1 only.
 
@@ -66,27 +68,43 @@ def max_over_ranks(x, ws):
     return float(t.item())
 
 
-def time_dominant_kernel(s, reps):
-    """Average duration of the fine-level Jacobi sweep (fea_mg_sweep, 4097^2) from HIP events
-    recorded on the stream the kernel is launched on."""
+def time_kernel(name, dtype, args, reps, stream):
+    """Average duration of one C-ABI kernel launch from HIP events recorded on its stream."""
     from feanet_amd import _lib
-    L0 = s.levels[0]
-    stream = torch.cuda.current_stream()
-    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab,
-            L0.B, L0.N, L0.ld, L0.bs, stream.cuda_stream)
     for _ in range(3):
-        _lib.call("mg_sweep", s.dtype, *args)
-    # one event pair per launch, recorded on the kernel's stream: the average duration of the kernel
+        _lib.call(name, dtype, *args, stream.cuda_stream)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for e0, e1 in ev:
         e0.record(stream)
-        _lib.call("mg_sweep", s.dtype, *args)
+        _lib.call(name, dtype, *args, stream.cuda_stream)
         e1.record(stream)
     ev[-1][1].synchronize()
-    t = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e-3
+    return sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e-3
+
+
+def time_fine_kernels(s, reps):
+    """The fine-level kernels at 4097^2: the north-star sweep (fea_mg_sweep, the `roofline` kernel) and
+    the two fused kernels the V-cycle actually runs on level 0 (sweep+residual+restriction,
+    prolongation+correction+sweep).  Returns {name: (seconds per launch, algorithmic bytes)}."""
+    L0, L1 = s.levels[0], s.levels[1]
+    st = torch.cuda.current_stream()
+    es = torch.finfo(s.dtype).bits // 8
     nodes = L0.B * (L0.N - 2) ** 2
-    bytes_per_launch = 24 * nodes  # read u, read f, write u' (fp64)
-    return t, bytes_per_launch
+    cnodes = L1.B * (L1.N - 2) ** 2
+    geom = (L0.B, L0.N, L0.ld, L0.bs)
+    kt, om, nt = s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab
+    out = {}
+    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, kt, om, nt) + geom
+    out["fea_mg_sweep"] = (time_kernel("mg_sweep", s.dtype, args, reps, st), 3 * es * nodes)
+    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), L1.f.data_ptr(), None, kt, om, nt,
+            s.rtab.data_ptr(), s.rtab.shape[0], s.w[0]) + geom + (L1.ld, L1.bs)
+    out["fea_mg_sweep_restrict"] = (time_kernel("mg_sweep_restrict", s.dtype, args, reps, st),
+                                    3 * es * nodes + es * cnodes)
+    args = (L0.a.data_ptr(), L1.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, None, kt, om, nt,
+            s.ptab.data_ptr(), s.ptab.shape[0], s.w[1]) + geom + (L1.ld, L1.bs)
+    out["fea_mg_prolong_sweep"] = (time_kernel("mg_prolong_sweep", s.dtype, args, reps, st),
+                                   3 * es * nodes + es * cnodes)
+    return out
 
 
 def load_traffic(kernel_key):
@@ -170,7 +188,8 @@ def main():
     dof = B * N * N * ws
     value = dof / (t / args.steps)
 
-    kt, kbytes = time_dominant_kernel(s, args.kernel_reps)
+    fine = time_fine_kernels(s, args.kernel_reps)
+    kt, kbytes = fine["fea_mg_sweep"]
     kt = max_over_ranks(kt, ws)
     achieved = kbytes / kt / 1e9
     traffic, tsrc = (load_traffic("mg_sweep_f64_4097") if (N == 4097 and B == 1 and args.dtype == "f64"
@@ -198,6 +217,9 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": kt * 1e6,
                      "algorithmic_bytes_per_launch": kbytes},
+        "fine_level_kernels": {k: {"avg_launch_us": t * 1e6, "algorithmic_bytes": nb,
+                                   "achieved_GBps": nb / t / 1e9, "frac": nb / t / 1e9 / HBM_PEAK_GBS}
+                               for k, (t, nb) in fine.items()},
         "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if ws == 1 else None,
         "vcycle_algorithmic_bytes": vbytes,
         "residual_contraction_per_cycle": conv,

@@ -73,15 +73,26 @@ __device__ __forceinline__ void vload(const T* p, T (&x)[V]) {
   }
 }
 
-template <typename T, int V>
+// NT: nontemporal (streaming) store — used on levels too large to be re-read from cache.  A
+// compile-time flag: with a runtime flag the two stores are merged before inlining and the
+// nontemporal hint is lost.
+template <typename T, int V, bool NT = false>
 __device__ __forceinline__ void vstore(T* p, const T (&x)[V]) {
+  constexpr bool nt = NT;
   if constexpr (V == 1) {
-    *p = x[0];
+    if constexpr (nt)
+      __builtin_nontemporal_store(x[0], p);
+    else
+      *p = x[0];
   } else {
     typename VecOf<T, V>::type v;
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = x[k];
-    *reinterpret_cast<typename VecOf<T, V>::type*>(p) = v;
+    auto* q = reinterpret_cast<typename VecOf<T, V>::type*>(p);
+    if constexpr (nt)
+      __builtin_nontemporal_store(v, q);
+    else
+      *q = v;
   }
 }
 
@@ -219,6 +230,7 @@ struct MgArgs {
   long long bsc;
   int nstrips, ntr;  // strips per row, row tasks per sample
   int rb;            // fine rows per row task (even)
+  int nt;            // nontemporal stores (level larger than FEANET_NT_BYTES)
 };
 
 struct TaskId {
@@ -255,10 +267,10 @@ __device__ __forceinline__ void load_tables(T* tab, const T* ktab, const T* omd,
     }
 }
 
-template <typename T, int V>
+template <typename T, int V, bool NT>
 __device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int N) {
   if (cl + V - 1 <= N - 2) {
-    vstore<T, V>(p, o);
+    vstore<T, V, NT>(p, o);
   } else {
 #pragma unroll
     for (int k = 0; k < V; ++k)
@@ -269,7 +281,7 @@ __device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int 
 // ---------------------------------------------------------------------------
 // Kernel A: interior Jacobi sweep  out = J(u, f);  ZERO: u == 0  ->  out = omd * f
 // ---------------------------------------------------------------------------
-template <typename T, bool MULTI, bool ZERO>
+template <typename T, bool MULTI, bool ZERO, bool NT>
 __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
@@ -311,7 +323,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
       if constexpr (MULTI) pload<V>(pb + ro, pv);
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = (MULTI ? tab[pv[k] * kTabStride + 9] : om) * fv[k];
-      store_masked<T, V>(ob + ro, o, cl, N);
+      store_masked<T, V, NT>(ob + ro, o, cl, N);
     }
   } else {
     Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
@@ -342,7 +354,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
         const T omk = MULTI ? tab[p1.a[k + 1] + 9] : om;
         o[k] = omk * (fx[k] - acc) + w1.a[k + 1];
       }
-      store_masked<T, V>(ob + rowo(r) + V * lane, o, cl, N);
+      store_masked<T, V, NT>(ob + rowo(r) + V * lane, o, cl, N);
       w0 = w1;
       w1 = w2;
       nx = nn;
@@ -361,7 +373,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
 // Kernel B: fused residual + restriction (+ optional zero-guess pre-sweep).
 //   task = (strip s, coarse rows [I0, I1)), fine rows 2I0-2 .. 2I1 are read.
 // ---------------------------------------------------------------------------
-template <typename T, bool MULTI, bool ZERO>
+template <typename T, bool MULTI, bool ZERO, bool NT>
 __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
@@ -454,7 +466,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
         T o[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) o[k] = w.u.a[k + 1];
-        store_masked<T, V>(vb + rowo(y) + V * lane, o, cl, N);
+        store_masked<T, V, NT>(vb + rowo(y) + V * lane, o, cl, N);
       }
     }
   };
@@ -514,7 +526,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     }
     T* cp = cb + (long long)(I + 1) * g.ldc;
     if (Jl + Q - 1 <= Nc - 2) {
-      vstore<T, Q>(cp, o);
+      vstore<T, Q, NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
@@ -617,7 +629,7 @@ __device__ __forceinline__ XPRow<V> xfinish(const XRawP<V>& r) {
 #ifndef FEA_SR_WAVES_PER_EU
 #define FEA_SR_WAVES_PER_EU 1  // forcing 3 (168 VGPRs) spills and measured slower (119 vs 107 us)
 #endif
-template <typename T, bool MULTI>
+template <typename T, bool MULTI, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 : FEA_SR_WAVES_PER_EU))) void k_mg_sweep_restrict(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
@@ -769,7 +781,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
       T o[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = w.a[k + 1];
-      store_masked<T, V>(ob + rowo(y) + V * lane, o, cl, N);
+      store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, N);
     }
   };
   const int ya = 2 * I0 - 1;  // first residual row
@@ -834,7 +846,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
     racc(acc, r, X4.p.w, 0, true);
     T* cp = cb + (long long)(I + 1) * g.ldc;
     if (Jl + Q - 1 <= Nc - 2) {
-      vstore<T, Q>(cp, o);
+      vstore<T, Q, NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
@@ -929,7 +941,7 @@ __device__ __forceinline__ void correct_odd(Row<T, V>& u, const CRow<T, V>& ca, 
   }
 }
 
-template <typename T, bool MULTI, bool SWEEP>
+template <typename T, bool MULTI, bool SWEEP, bool NT>
 __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
@@ -1002,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = b.a[k + 1];
     }
-    store_masked<T, V>(ob + rowo(y) + V * lane, o, cl, N);
+    store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, N);
   };
 
   // window rows r0-1 (even, coarse a0) and r0 (odd, coarse a0, a0+1)
@@ -1165,12 +1177,10 @@ static inline bool mg_n_ok(int N) {
 
 // Rows per wave task: the largest even count (<= kRB) that still gives >= kTargetWaves waves,
 // so small levels are spread over the chip instead of being marched row by row by a few waves.
+// (tuning knobs are read at every launch so one process can A/B them; graphs capture the choice)
 static int target_waves() {
-  static const int tw = [] {
-    const char* e = getenv("FEANET_TARGET_WAVES");  // tuning knob (default 2048 = 8 waves per CU)
-    return e ? std::max(64, atoi(e)) : 2048;
-  }();
-  return tw;
+  const char* e = getenv("FEANET_TARGET_WAVES");  // default 2048 = 8 waves per CU
+  return e ? std::max(64, atoi(e)) : 2048;
 }
 static inline int pick_rb(int B, int nstrips, int rows) {
   const int tw = target_waves();
@@ -1179,9 +1189,17 @@ static inline int pick_rb(int B, int nstrips, int rows) {
   return 2;
 }
 
+// Levels whose fields exceed this many bytes stream their stores past the caches (measured on the
+// 4097^2 fp64 sweep: 64.8 us with nontemporal stores vs 84.6 us without)
+static long long nt_bytes() {
+  const char* e = getenv("FEANET_NT_BYTES");
+  return e ? atoll(e) : (32ll << 20);
+}
+
 template <typename T>
 static MgArgs<T> mg_args(int N, int ld, long long bs, int B) {
   MgArgs<T> g{};
+  g.nt = (long long)B * bs * (long long)sizeof(T) > nt_bytes();
   g.N = N;
   g.ld = ld;
   g.bs = bs;
@@ -1248,11 +1266,11 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (!u) {                                                                                                \
-      if (multi) k_mg_sweep<T, true, true><<<grid, 256, 0, s>>>(g);                                          \
-      else k_mg_sweep<T, false, true><<<grid, 256, 0, s>>>(g);                                               \
+      if (multi) { if (g.nt) k_mg_sweep<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                          \
+      else { if (g.nt) k_mg_sweep<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                               \
     } else {                                                                                                 \
-      if (multi) k_mg_sweep<T, true, false><<<grid, 256, 0, s>>>(g);                                         \
-      else k_mg_sweep<T, false, false><<<grid, 256, 0, s>>>(g);                                              \
+      if (multi) { if (g.nt) k_mg_sweep<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                         \
+      else { if (g.nt) k_mg_sweep<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                              \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
@@ -1275,11 +1293,11 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
     const bool multi = ntab > 1;                                                                             \
     if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
     if (!u) {                                                                                                \
-      if (multi) k_mg_resid_restrict<T, true, true><<<grid, 256, 0, s>>>(g);                                 \
-      else k_mg_resid_restrict<T, false, true><<<grid, 256, 0, s>>>(g);                                      \
+      if (multi) { if (g.nt) k_mg_resid_restrict<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                 \
+      else { if (g.nt) k_mg_resid_restrict<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                      \
     } else {                                                                                                 \
-      if (multi) k_mg_resid_restrict<T, true, false><<<grid, 256, 0, s>>>(g);                                \
-      else k_mg_resid_restrict<T, false, false><<<grid, 256, 0, s>>>(g);                                     \
+      if (multi) { if (g.nt) k_mg_resid_restrict<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                \
+      else { if (g.nt) k_mg_resid_restrict<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                     \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
@@ -1300,8 +1318,8 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
     g.ntr = div_up(Nc - 2, g.rb / 2);                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (ntab > 1) k_mg_sweep_restrict<T, true><<<grid, 256, 0, s>>>(g);                                      \
-    else k_mg_sweep_restrict<T, false><<<grid, 256, 0, s>>>(g);                                              \
+    if (ntab > 1) { if (g.nt) k_mg_sweep_restrict<T, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep_restrict<T, true, false><<<grid, 256, 0, s>>>(g); }                                      \
+    else { if (g.nt) k_mg_sweep_restrict<T, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep_restrict<T, false, false><<<grid, 256, 0, s>>>(g); }                                              \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \
@@ -1322,11 +1340,11 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (sweep) {                                                                                             \
-      if (multi) k_mg_prolong<T, true, true><<<grid, 256, 0, s>>>(g);                                        \
-      else k_mg_prolong<T, false, true><<<grid, 256, 0, s>>>(g);                                             \
+      if (multi) { if (g.nt) k_mg_prolong<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                        \
+      else { if (g.nt) k_mg_prolong<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                             \
     } else {                                                                                                 \
-      if (multi) k_mg_prolong<T, true, false><<<grid, 256, 0, s>>>(g);                                       \
-      else k_mg_prolong<T, false, false><<<grid, 256, 0, s>>>(g);                                            \
+      if (multi) { if (g.nt) k_mg_prolong<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                       \
+      else { if (g.nt) k_mg_prolong<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                            \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \

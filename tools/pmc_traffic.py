@@ -27,7 +27,7 @@ def short(n):
     return n.replace("void ", "").replace("fea::", "").split("(")[0]
 
 
-def main(fcsv, wcsv, out_json, summary=None):
+def main(fcsv, wcsv, out_json, summary=None, src="profiles/r01_pmc"):
     fetch = load(fcsv, "FETCH_SIZE")
     write = load(wcsv, "WRITE_SIZE")
     rows = []
@@ -38,13 +38,13 @@ def main(fcsv, wcsv, out_json, summary=None):
         rows.append((short(name), grid, len(fetch[key]), f, w))
     res = {}
     for name, grid, n, f, w in rows:
-        if name == "k_mg_sweep<double, false, false>" and grid == 262144:
+        if name.startswith("k_mg_sweep<double, false, false") and grid == 262144:
             nodes = 4095 * 4095
             res["mg_sweep_f64_4097"] = {
                 "hbm_bytes_per_launch": f + w, "read_bytes_per_launch": f, "write_bytes_per_launch": w,
                 "algorithmic_bytes_per_launch": 24 * nodes, "launches": n,
                 "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads), KiB -> bytes",
-                "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (profiles/r01_pmc)"}
+                "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({src})"}
     json.dump(res, open(out_json, "w"), indent=1)
     if summary:
         with open(summary, "w") as fh:
