@@ -89,9 +89,9 @@ def time_fine_kernels(s, reps):
     L0, L1 = s.levels[0], s.levels[1]
     st = torch.cuda.current_stream()
     es = torch.finfo(s.dtype).bits // 8
-    nodes = L0.B * (L0.N - 2) ** 2
-    cnodes = L1.B * (L1.N - 2) ** 2
-    geom = (L0.B, L0.N, L0.ld, L0.bs)
+    nodes = L0.B * (L0.H - 2) * (L0.W - 2)
+    cnodes = L1.B * (L1.H - 2) * (L1.W - 2)
+    geom = L0.geom()
     kt, om, nt = s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab
     out = {}
     args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, kt, om, nt) + geom

@@ -26,7 +26,7 @@
  *      boundary used by the FEANet.* shim modules (KNet/FNet/JacobiBlock/MultiGrid).
  *  (2) "mg" ops on FRAMED level buffers owned by the MultigridSolver: node (r, c)
  *      of sample b lives at  base[b*bstride + (r+1)*ld + (A-1) + c],  A = 128/sizeof(T)
- *      (so column 1 starts a 128-byte line), with a zero ghost ring at r,c = -1 and N.
+ *      (so column 1 starts a 128-byte line), with a ghost ring at r = -1, H and c = -1, W.
  *      Use fea_mg_layout() for ld / bstride.  Boundary nodes hold the Dirichlet values
  *      and are never written by mg kernels (SURVEY §8a A9 invariant).
  */
@@ -46,16 +46,16 @@ extern "C" {
 /* ---------------------------------------------------------------------------
  * Library / layout queries
  * ------------------------------------------------------------------------- */
-/* ABI version (bumped on any signature change). */
+/* ABI version (bumped on any signature change; 2 = H x W framed grids). */
 int fea_abi_version(void);
 
-/* Framed layout of an N x N level for elements of `elem_size` bytes (4 or 8):
+/* Framed layout of an H x W level for elements of `elem_size` bytes (4 or 8):
  * writes the row pitch (elements) and the per-sample stride (elements).
- * Returns 0, or FEA_EINVAL for unsupported N / elem_size. */
-int fea_mg_layout(int N, int elem_size, int* ld, long long* bstride);
+ * Returns 0, or FEA_EINVAL for unsupported H, W / elem_size. */
+int fea_mg_layout(int H, int W, int elem_size, int* ld, long long* bstride);
 
 /* Bytes of double workspace needed by the norm kernels for this shape. */
-size_t fea_norm_workspace_bytes(int B, int N);
+size_t fea_norm_workspace_bytes(int B, int H, int W);
 
 /* ---------------------------------------------------------------------------
  * (1) Generic ops, contiguous [B, C, H, W]
@@ -116,7 +116,7 @@ int fea_prolong_f64(const double* e, int C, double* out, const double* add, cons
 
 /* out[b] = || r[b, 0, 1:-1, 1:-1] ||_2 with r = f - K u (u may be the residual itself: pass
  * f = NULL and ktab = NULL to take the norm of u).  Deterministic two-pass reduction; ws must
- * hold fea_norm_workspace_bytes(B, max(H, W)) bytes.  Replaces the drivers'
+ * hold fea_norm_workspace_bytes(B, H, W) bytes.  Replaces the drivers'
  * torch.norm(residual[:, :, 1:-1, 1:-1], dim=(2,3)) (M-FEANet-mg_test.ipynb:27428-27429). */
 int fea_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, const float* ktab, int ntab,
                           double* out, double* ws, int B, int H, int W, void* stream);
@@ -124,27 +124,28 @@ int fea_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, 
                           double* out, double* ws, int B, int H, int W, void* stream);
 
 /* ---------------------------------------------------------------------------
- * (2) Framed multigrid-level ops (MultigridSolver), square N x N, N = 2^k + 1 >= 5.
+ * (2) Framed multigrid-level ops (MultigridSolver), H x W grids (H, W >= 3; the intergrid ops need
+ *     odd H and W: the coarse grid is (H+1)/2 x (W+1)/2, fine nodes (2I, 2J) on coarse (I, J)).
  *     `pid`/`pidc` are framed uint8 maps with the same ld (in bytes) as the T fields.
  * ------------------------------------------------------------------------- */
 
-/* contiguous [B,1,N,N] -> framed, applying u*geo + bc (geo NULL: square, bc NULL: zero) */
+/* contiguous [B,1,H,W] -> framed, applying u*geo + bc (geo NULL: square, bc NULL: zero) */
 int fea_mg_pack_f32(const float* src, float* dst, const float* geo, long long geo_bstride,
-                    const float* bc, long long bc_bstride, int B, int N, int ld, long long bstride,
+                    const float* bc, long long bc_bstride, int B, int H, int W, int ld, long long bstride,
                     void* stream);
 int fea_mg_pack_f64(const double* src, double* dst, const double* geo, long long geo_bstride,
-                    const double* bc, long long bc_bstride, int B, int N, int ld, long long bstride,
+                    const double* bc, long long bc_bstride, int B, int H, int W, int ld, long long bstride,
                     void* stream);
-/* framed -> contiguous [B,1,N,N] */
-int fea_mg_unpack_f32(const float* src, float* dst, int B, int N, int ld, long long bstride, void* stream);
-int fea_mg_unpack_f64(const double* src, double* dst, int B, int N, int ld, long long bstride, void* stream);
+/* framed -> contiguous [B,1,H,W] */
+int fea_mg_unpack_f32(const float* src, float* dst, int B, int H, int W, int ld, long long bstride, void* stream);
+int fea_mg_unpack_f64(const double* src, double* dst, int B, int H, int W, int ld, long long bstride, void* stream);
 
 /* Interior sweep out = J(u, f) (boundary untouched).  u == NULL: zero initial guess
  * (out = omd*f), the coarse-level pre-smooth of MultiGrid.iterate (FEANet/multigrid.py:171-172). */
 int fea_mg_sweep_f32(const float* u, const float* f, float* out, const uint8_t* pid, const float* ktab,
-                     const float* omd, int ntab, int B, int N, int ld, long long bstride, void* stream);
+                     const float* omd, int ntab, int B, int H, int W, int ld, long long bstride, void* stream);
 int fea_mg_sweep_f64(const double* u, const double* f, double* out, const uint8_t* pid, const double* ktab,
-                     const double* omd, int ntab, int B, int N, int ld, long long bstride, void* stream);
+                     const double* omd, int ntab, int B, int H, int W, int ld, long long bstride, void* stream);
 
 /* Fused residual + restriction: fc(interior) = w0 * R(f - K u), kernel by fine-node pattern.
  * u == NULL: zero-initial-guess mode — the kernel first forms v = omd*f (the coarse-level
@@ -152,11 +153,11 @@ int fea_mg_sweep_f64(const double* u, const double* f, double* out, const uint8_
  * FEANet/multigrid.py:171-172 then :168-170).  (ldc, bstridec) = coarse layout. */
 int fea_mg_residual_restrict_f32(const float* u, const float* f, float* v_out, float* fc, const uint8_t* pid,
                                  const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
-                                 float w0, int B, int N, int ld, long long bstride, int ldc,
+                                 float w0, int B, int H, int W, int ld, long long bstride, int ldc,
                                  long long bstridec, void* stream);
 int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out, double* fc,
                                  const uint8_t* pid, const double* ktab, const double* omd, int ntab,
-                                 const double* rtab, int nrtab, double w0, int B, int N, int ld,
+                                 const double* rtab, int nrtab, double w0, int B, int H, int W, int ld,
                                  long long bstride, int ldc, long long bstridec, void* stream);
 
 /* Fused pre-smooth + residual + restriction on a level with a given iterate (temporal blocking):
@@ -164,11 +165,11 @@ int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out
  * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357). */
 int fea_mg_sweep_restrict_f32(const float* u, const float* f, float* u_out, float* fc, const uint8_t* pid,
                               const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
-                              float w0, int B, int N, int ld, long long bstride, int ldc, long long bstridec,
+                              float w0, int B, int H, int W, int ld, long long bstride, int ldc, long long bstridec,
                               void* stream);
 int fea_mg_sweep_restrict_f64(const double* u, const double* f, double* u_out, double* fc, const uint8_t* pid,
                               const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
-                              double w0, int B, int N, int ld, long long bstride, int ldc, long long bstridec,
+                              double w0, int B, int H, int W, int ld, long long bstride, int ldc, long long bstridec,
                               void* stream);
 
 /* Fused prolongation + correction + post-sweep:
@@ -176,44 +177,49 @@ int fea_mg_sweep_restrict_f64(const double* u, const double* f, double* u_out, d
  * FEANet/multigrid.py:177-181 (Interpolate, add, Relax) in one pass. */
 int fea_mg_prolong_sweep_f32(const float* u, const float* ec, const float* f, float* out, const uint8_t* pid,
                              const uint8_t* pidc, const float* ktab, const float* omd, int ntab,
-                             const float* ptab, int nptab, float w1, int B, int N, int ld, long long bstride,
+                             const float* ptab, int nptab, float w1, int B, int H, int W, int ld, long long bstride,
                              int ldc, long long bstridec, void* stream);
 int fea_mg_prolong_sweep_f64(const double* u, const double* ec, const double* f, double* out,
                              const uint8_t* pid, const uint8_t* pidc, const double* ktab, const double* omd,
-                             int ntab, const double* ptab, int nptab, double w1, int B, int N, int ld,
+                             int ntab, const double* ptab, int nptab, double w1, int B, int H, int W, int ld,
                              long long bstride, int ldc, long long bstridec, void* stream);
 
 /* Prolongation + correction without a sweep (nu2 = 0 schedules): out = u + w1 * P(ec), interior. */
 int fea_mg_prolong_add_f32(const float* u, const float* ec, float* out, const uint8_t* pidc, const float* ptab,
-                           int nptab, float w1, int B, int N, int ld, long long bstride, int ldc,
+                           int nptab, float w1, int B, int H, int W, int ld, long long bstride, int ldc,
                            long long bstridec, void* stream);
 int fea_mg_prolong_add_f64(const double* u, const double* ec, double* out, const uint8_t* pidc,
-                           const double* ptab, int nptab, double w1, int B, int N, int ld, long long bstride,
+                           const double* ptab, int nptab, double w1, int B, int H, int W, int ld, long long bstride,
                            int ldc, long long bstridec, void* stream);
 
-/* out[b] = || (f - K u)[b, 1:-1, 1:-1] ||_2, deterministic; ws >= fea_norm_workspace_bytes(B, N). */
+/* out[b] = || (f - K u)[b, rlo:rhi, 1:-1] ||_2 (rows rlo..rhi-1; rlo = rhi = 0: all interior rows,
+ * the drivers' [1:-1, 1:-1]), deterministic; ws >= fea_norm_workspace_bytes(B, H, W).  A row range
+ * gives a domain-decomposed rank the sum over the rows it owns. */
 int fea_mg_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, const float* ktab, int ntab,
-                             double* out, double* ws, int B, int N, int ld, long long bstride, void* stream);
+                             double* out, double* ws, int B, int H, int W, int ld, long long bstride, int rlo,
+                             int rhi, void* stream);
 int fea_mg_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
-                             double* out, double* ws, int B, int N, int ld, long long bstride, void* stream);
+                             double* out, double* ws, int B, int H, int W, int ld, long long bstride, int rlo,
+                             int rhi, void* stream);
 
-/* The whole coarse end of the V-cycle (levels t..t+nlev-1, N_t = 2^k + 1 <= 65) in ONE launch,
+/* The whole coarse end of the V-cycle (levels t..t+nlev-1 of an Ht x Wt level, Ht, Wt <= 65 and
+ * (Ht-1), (Wt-1) divisible by 2^(nlev-1)) in ONE launch,
  * one 1024-thread workgroup per sample, every level resident in LDS.  Input f_t and output v_t
  * are framed level-t buffers (ld_t, bs_t); v_t's interior is written.  The sub-cycle starts from a
  * zero guess: nu1 pre-sweeps per level (none if q2), nu1+nu2 (q2: nu2) sweeps on the coarsest,
  * prolongation + correction + nu2 post-sweeps (FEANet/multigrid.py:165-183 below level t).
- * pid_levels: the nlev compact N_k x N_k uint8 pattern maps concatenated (NULL when ntab == 1);
+ * pid_levels: the nlev compact H_k x W_k uint8 pattern maps concatenated (NULL when ntab == 1);
  * rtab/ptab hold ntab kernels (broadcast single kernels on the host). */
-int fea_mg_coarse_tail_f32(const float* f_t, float* v_t, int Nt, int nlev, int ld_t, long long bs_t,
+int fea_mg_coarse_tail_f32(const float* f_t, float* v_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
                            const uint8_t* pid_levels, const float* ktab, const float* omd, int ntab,
                            const float* rtab, const float* ptab, float w0, float w1, int nu1, int nu2, int q2,
                            int B, void* stream);
-int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Nt, int nlev, int ld_t, long long bs_t,
+int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
                            const uint8_t* pid_levels, const double* ktab, const double* omd, int ntab,
                            const double* rtab, const double* ptab, double w0, double w1, int nu1, int nu2,
                            int q2, int B, void* stream);
-/* LDS bytes the coarse tail needs for (Nt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
-size_t fea_mg_coarse_tail_lds_bytes(int Nt, int nlev, int elem_size, int multi);
+/* LDS bytes the coarse tail needs for (Ht, Wt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
+size_t fea_mg_coarse_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi);
 
 #ifdef __cplusplus
 }

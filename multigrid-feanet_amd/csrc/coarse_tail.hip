@@ -1,4 +1,4 @@
-// coarse_tail.hip — the coarse end of the V-cycle (levels with N <= 65) in ONE launch.
+// coarse_tail.hip — the coarse end of the V-cycle (levels with H, W <= 65) in ONE launch.
 //
 // Below ~129^2 nodes a level's kernels are pure launch/latency cost (each level is a few
 // microseconds of work spread thin over the chip, twice per V-cycle).  Here one 1024-thread
@@ -17,7 +17,7 @@ namespace fea {
 
 constexpr int kTailThreads = 1024;
 constexpr int kTailMaxLevels = 8;
-constexpr int kTailMaxN = 65;
+constexpr int kTailMaxN = 65;  // per dimension
 constexpr int kTailLdsBytes = 160 * 1024 - 1024;
 constexpr int kTS = 10;  // table stride (9 weights + omega/d)
 
@@ -31,34 +31,30 @@ struct TailArgs {
   const T* rtab;
   const T* ptab;
   T w0, w1;
-  int Nt, nlev, ld_t;
+  int Ht, Wt, nlev, ld_t;
   long long bs_t;
   int ntab, nu1, nu2, q2;
 };
 
-template <typename T>
-__host__ __device__ inline long long tail_elems(int Nt, int nlev) {
+__host__ __device__ inline long long tail_elems(int Ht, int Wt, int nlev) {
   long long s = 0;
-  for (int k = 0, N = Nt; k < nlev; ++k, N = (N + 1) / 2) s += (long long)N * N;
+  for (int k = 0, H = Ht, W = Wt; k < nlev; ++k, H = (H + 1) / 2, W = (W + 1) / 2) s += (long long)H * W;
   return s;
 }
 
 template <typename T>
-__host__ __device__ inline long long tail_lds_bytes(int Nt, int nlev, bool multi) {
-  const long long e = tail_elems<T>(Nt, nlev);
+__host__ __device__ inline long long tail_lds_bytes(int Ht, int Wt, int nlev, bool multi) {
+  const long long e = tail_elems(Ht, Wt, nlev);
   long long b = 3 * e * (long long)sizeof(T);
   if (multi) b += (e + 15) / 16 * 16;
   b += 3LL * FEA_MAX_PATTERNS * kTS * sizeof(T);
   return b;
 }
 
-__device__ __forceinline__ int tail_N(int Nt, int k) { return ((Nt - 1) >> k) + 1; }
-__device__ __forceinline__ int tail_off(int Nt, int k) {  // element offset of level k in a region
+__device__ __forceinline__ int tail_n(int n0, int k) { return ((n0 - 1) >> k) + 1; }
+__device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element offset of level k in a region
   int o = 0;
-  for (int j = 0; j < k; ++j) {
-    const int n = tail_N(Nt, j);
-    o += n * n;
-  }
+  for (int j = 0; j < k; ++j) o += tail_n(Ht, j) * tail_n(Wt, j);
   return o;
 }
 
@@ -66,8 +62,8 @@ template <typename T, bool MULTI>
 __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kTailLdsBytes];
   const int tid = threadIdx.x;
-  const int nlev = a.nlev, Nt = a.Nt;
-  const int tot = tail_off(Nt, nlev);
+  const int nlev = a.nlev, Ht = a.Ht, Wt = a.Wt;
+  const int tot = tail_off(Ht, Wt, nlev);
   T* va = reinterpret_cast<T*>(smem);
   T* vb = va + tot;
   T* fs = vb + tot;
@@ -89,8 +85,8 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     for (int i = tid; i < tot; i += kTailThreads) pl[i] = a.pid[i];
   {
     const T* src = a.f_t + (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1);
-    for (int i = tid; i < Nt * Nt; i += kTailThreads) {
-      const int r = i / Nt, c = i - r * Nt;
+    for (int i = tid; i < Ht * Wt; i += kTailThreads) {
+      const int r = i / Wt, c = i - r * Wt;
       fs[i] = src[(long long)(r + 1) * a.ld_t + c];
     }
   }
@@ -98,7 +94,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
 
   // pattern offset (into a stride-10 table) of node j of a level whose map starts at pk
   auto P = [&](const uint8_t* pk, int j) -> int { return MULTI ? pk[j] * kTS : 0; };
-  auto Ku = [&](int N, const uint8_t* pk, const T* u, int r, int c) -> T {
+  auto Ku = [&](int N, const uint8_t* pk, const T* u, int r, int c) -> T {  // N = row pitch (W)
     const int i0 = (r - 1) * N + c - 1;
     T acc = 0;
 #pragma unroll
@@ -110,26 +106,26 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
       }
     return acc;
   };
-  auto sweep = [&](int N, const uint8_t* pk, const T* f, const T* src, T* dst, bool zero) {
+  auto sweep = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst, bool zero) {
     const int m = N - 2;
-    for (int q = tid; q < m * m; q += kTailThreads) {
+    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
       const int r = 1 + q / m, c = 1 + q % m, i = r * N + c;
       const T om = ktb[P(pk, i) + 9];
       dst[i] = zero ? om * f[i] : om * (f[i] - Ku(N, pk, src, r, c)) + src[i];
     }
     __syncthreads();
   };
-  auto residual = [&](int N, const uint8_t* pk, const T* f, const T* src, T* dst) {
+  auto residual = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst) {
     const int m = N - 2;
-    for (int q = tid; q < m * m; q += kTailThreads) {
+    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
       const int r = 1 + q / m, c = 1 + q % m;
       dst[r * N + c] = f[r * N + c] - Ku(N, pk, src, r, c);
     }
     __syncthreads();
   };
-  auto restrict_ = [&](int N, const uint8_t* pk, const T* res, T* fc) {  // fine residual -> coarse f
-    const int Nc = (N + 1) / 2, m = Nc - 2;
-    for (int q = tid; q < m * m; q += kTailThreads) {
+  auto restrict_ = [&](int H, int N, const uint8_t* pk, const T* res, T* fc) {  // fine residual -> coarse f
+    const int Nc = (N + 1) / 2, m = Nc - 2, mh = (H + 1) / 2 - 2;
+    for (int q = tid; q < mh * m; q += kTailThreads) {
       const int I = 1 + q / m, J = 1 + q % m;
       T acc = 0;
 #pragma unroll
@@ -143,9 +139,9 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     }
     __syncthreads();
   };
-  auto prolong_add = [&](int N, const uint8_t* pkc, T* v, const T* e) {  // v += w1 P e, interior
+  auto prolong_add = [&](int H, int N, const uint8_t* pkc, T* v, const T* e) {  // v += w1 P e, interior
     const int Nc = (N + 1) / 2, m = N - 2;
-    for (int q = tid; q < m * m; q += kTailThreads) {
+    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
       const int y = 1 + q / m, x = 1 + q % m;
       T acc = 0;
 #pragma unroll
@@ -166,50 +162,51 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
   };
 
   unsigned cur = 0;  // bit k set: level k's current iterate is in vb
-  auto curp = [&](int k) -> T* { return ((cur >> k) & 1u) ? vb + tail_off(Nt, k) : va + tail_off(Nt, k); };
-  auto othp = [&](int k) -> T* { return ((cur >> k) & 1u) ? va + tail_off(Nt, k) : vb + tail_off(Nt, k); };
+  auto off = [&](int k) { return tail_off(Ht, Wt, k); };
+  auto curp = [&](int k) -> T* { return ((cur >> k) & 1u) ? vb + off(k) : va + off(k); };
+  auto othp = [&](int k) -> T* { return ((cur >> k) & 1u) ? va + off(k) : vb + off(k); };
   auto flip = [&](int k) { cur ^= (1u << k); };
-  auto fp = [&](int k) -> T* { return fs + tail_off(Nt, k); };
-  auto pp = [&](int k) -> const uint8_t* { return pl + tail_off(Nt, k); };
+  auto fp = [&](int k) -> T* { return fs + off(k); };
+  auto pp = [&](int k) -> const uint8_t* { return pl + off(k); };
 
   const bool presmooth = a.nu1 > 0 && !a.q2;
   for (int k = 0; k + 1 < nlev; ++k) {
-    const int N = tail_N(Nt, k);
+    const int H = tail_n(Ht, k), N = tail_n(Wt, k);
     if (presmooth) {
-      sweep(N, pp(k), fp(k), nullptr, curp(k), true);
+      sweep(H, N, pp(k), fp(k), nullptr, curp(k), true);
       for (int s = 1; s < a.nu1; ++s) {
-        sweep(N, pp(k), fp(k), curp(k), othp(k), false);
+        sweep(H, N, pp(k), fp(k), curp(k), othp(k), false);
         flip(k);
       }
     }
-    residual(N, pp(k), fp(k), curp(k), othp(k));
-    restrict_(N, pp(k), othp(k), fp(k + 1));
+    residual(H, N, pp(k), fp(k), curp(k), othp(k));
+    restrict_(H, N, pp(k), othp(k), fp(k + 1));
   }
   {
-    const int k = nlev - 1, N = tail_N(Nt, k);
+    const int k = nlev - 1, H = tail_n(Ht, k), N = tail_n(Wt, k);
     const int ncs = a.q2 ? a.nu2 : a.nu1 + a.nu2;
     if (ncs > 0) {
-      sweep(N, pp(k), fp(k), nullptr, curp(k), true);
+      sweep(H, N, pp(k), fp(k), nullptr, curp(k), true);
       for (int s = 1; s < ncs; ++s) {
-        sweep(N, pp(k), fp(k), curp(k), othp(k), false);
+        sweep(H, N, pp(k), fp(k), curp(k), othp(k), false);
         flip(k);
       }
     }
   }
   for (int k = nlev - 2; k >= 0; --k) {
-    const int N = tail_N(Nt, k);
-    prolong_add(N, pp(k + 1), curp(k), curp(k + 1));
+    const int H = tail_n(Ht, k), N = tail_n(Wt, k);
+    prolong_add(H, N, pp(k + 1), curp(k), curp(k + 1));
     for (int s = 0; s < a.nu2; ++s) {
-      sweep(N, pp(k), fp(k), curp(k), othp(k), false);
+      sweep(H, N, pp(k), fp(k), curp(k), othp(k), false);
       flip(k);
     }
   }
   {
     const T* v = curp(0);
     T* dst = a.v_t + (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1);
-    for (int i = tid; i < Nt * Nt; i += kTailThreads) {
-      const int r = i / Nt, c = i - r * Nt;
-      if (r > 0 && r < Nt - 1 && c > 0 && c < Nt - 1) dst[(long long)(r + 1) * a.ld_t + c] = v[i];
+    for (int i = tid; i < Ht * Wt; i += kTailThreads) {
+      const int r = i / Wt, c = i - r * Wt;
+      if (r > 0 && r < Ht - 1 && c > 0 && c < Wt - 1) dst[(long long)(r + 1) * a.ld_t + c] = v[i];
     }
   }
 }
@@ -218,29 +215,37 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
 
 using namespace fea;
 
-extern "C" size_t fea_mg_coarse_tail_lds_bytes(int Nt, int nlev, int elem_size, int multi) {
-  if (Nt < 3 || nlev < 1 || nlev > kTailMaxLevels) return 0;
-  return elem_size == 8 ? (size_t)tail_lds_bytes<double>(Nt, nlev, multi != 0)
-                        : (size_t)tail_lds_bytes<float>(Nt, nlev, multi != 0);
+extern "C" size_t fea_mg_coarse_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi) {
+  if (Ht < 3 || Wt < 3 || nlev < 1 || nlev > kTailMaxLevels) return 0;
+  return elem_size == 8 ? (size_t)tail_lds_bytes<double>(Ht, Wt, nlev, multi != 0)
+                        : (size_t)tail_lds_bytes<float>(Ht, Wt, nlev, multi != 0);
+}
+
+// (n - 1) divisible by 2^(nlev-1) and every level >= 3 nodes
+static inline bool tail_dim_ok(int n, int nlev) {
+  if (n < 3 || n > kTailMaxN) return false;
+  for (int k = 1; k < nlev; ++k) {
+    if ((n - 1) & 1) return false;
+    n = (n + 1) / 2;
+    if (n < 3) return false;
+  }
+  return true;
 }
 
 #define FEA_TAIL_API(SUF, T)                                                                                  \
-  extern "C" int fea_mg_coarse_tail_##SUF(const T* f_t, T* v_t, int Nt, int nlev, int ld_t, long long bs_t,   \
+  extern "C" int fea_mg_coarse_tail_##SUF(const T* f_t, T* v_t, int Ht, int Wt, int nlev, int ld_t,          \
+                                          long long bs_t,                                                      \
                                           const uint8_t* pid_levels, const T* ktab, const T* omd, int ntab,    \
                                           const T* rtab, const T* ptab, T w0, T w1, int nu1, int nu2, int q2,  \
                                           int B, void* stream) {                                               \
     if (!f_t || !v_t || !ktab || !omd || !rtab || !ptab || B <= 0 || nlev < 1 || nlev > kTailMaxLevels)       \
       return FEA_EINVAL;                                                                                      \
-    if (Nt < 3 || Nt > kTailMaxN || ((Nt - 1) & (Nt - 2)) != 0 || nu1 < 0 || nu2 < 0) return FEA_EINVAL;      \
-    int N = Nt;                                                                                               \
-    for (int k = 1; k < nlev; ++k) {                                                                          \
-      N = (N + 1) / 2;                                                                                        \
-      if (N < 3) return FEA_EINVAL;                                                                           \
-    }                                                                                                         \
+    if (!tail_dim_ok(Ht, nlev) || !tail_dim_ok(Wt, nlev) || nu1 < 0 || nu2 < 0) return FEA_EINVAL;           \
     const bool multi = ntab > 1;                                                                              \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (multi && !pid_levels)) return FEA_EINVAL;                     \
-    if (tail_lds_bytes<T>(Nt, nlev, multi) > kTailLdsBytes) return FEA_EINVAL;                                \
-    TailArgs<T> a{f_t, v_t, pid_levels, ktab, omd, rtab, ptab, w0, w1, Nt, nlev, ld_t, bs_t, ntab, nu1, nu2, q2}; \
+    if (tail_lds_bytes<T>(Ht, Wt, nlev, multi) > kTailLdsBytes) return FEA_EINVAL;                           \
+    TailArgs<T> a{f_t, v_t, pid_levels, ktab, omd, rtab, ptab, w0, w1, Ht, Wt, nlev, ld_t, bs_t, ntab, nu1, nu2,  \
+                  q2};                                                                                        \
     if (multi) k_mg_coarse_tail<T, true><<<B, kTailThreads, 0, (hipStream_t)stream>>>(a);                     \
     else k_mg_coarse_tail<T, false><<<B, kTailThreads, 0, (hipStream_t)stream>>>(a);                          \
     FEA_LAUNCH_CHECK();                                                                                       \

@@ -38,17 +38,19 @@ constexpr int kTabStride = 10;  // LDS table row: 9 stencil weights + omega/d
 static inline int div_up(int a, int b) { return (a + b - 1) / b; }
 
 template <typename T>
-static inline int mg_nstrips(int N) { return div_up(N - 2, Frame<T>::SW); }
+static inline int mg_nstrips(int W) { return div_up(W - 2, Frame<T>::SW); }
 
+// row pitch (elements) of a framed grid with W columns
 template <typename T>
-static inline int mg_ld(int N) {
+static inline int mg_ld(int W) {
   using F = Frame<T>;
-  const int need = F::OFF + 2 + std::max(mg_nstrips<T>(N) * F::SW + F::VEC, N + F::SW / 2 + 1);
+  const int need = F::OFF + 2 + std::max(mg_nstrips<T>(W) * F::SW + F::VEC, W + F::SW / 2 + 1);
   return div_up(need, F::A) * F::A;
 }
 
+// sample pitch of an H x W framed grid: H rows plus the ghost rows -1 and H
 template <typename T>
-static inline long long mg_bstride(int N) { return (long long)(N + 2) * mg_ld<T>(N); }
+static inline long long mg_bstride(int H, int W) { return (long long)(H + 2) * mg_ld<T>(W); }
 
 // ---------------------------------------------------------------------------
 // vector access helpers
@@ -224,12 +226,13 @@ struct MgArgs {
   double* part;
   int ntab, nrtab, nptab;
   T w;
-  int N, ld;
+  int H, W, ld;  // rows, columns of the (local) grid
   long long bs;
-  int Nc, ldc;
+  int Hc, Wc, ldc;
   long long bsc;
   int nstrips, ntr;  // strips per row, row tasks per sample
   int rb;            // fine rows per row task (even)
+  int rlo, rhi;      // row range of the residual norm
   int nt;            // nontemporal stores (level larger than FEANET_NT_BYTES)
 };
 
@@ -268,13 +271,13 @@ __device__ __forceinline__ void load_tables(T* tab, const T* ktab, const T* omd,
 }
 
 template <typename T, int V, bool NT>
-__device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int N) {
-  if (cl + V - 1 <= N - 2) {
+__device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int W) {
+  if (cl + V - 1 <= W - 2) {
     vstore<T, V, NT>(p, o);
   } else {
 #pragma unroll
     for (int k = 0; k < V; ++k)
-      if (cl + k <= N - 2) p[k] = o[k];
+      if (cl + k <= W - 2) p[k] = o[k];
   }
 }
 
@@ -293,10 +296,10 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N;
+  const int H = g.H, W = g.W;
   const int c0 = 1 + id.s * F::SW;
   const int r0 = 1 + id.t * g.rb;
-  const int r1 = min(r0 + g.rb, N - 1);
+  const int r1 = min(r0 + g.rb, H - 1);
   const int cl = c0 + V * lane;  // first own column
   T ks[9];
   T om = 0;
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   T* __restrict__ ob = g.out + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;  // pattern maps: one per mesh
   const int ld = g.ld;
-  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, H) + 1) * ld; };
 
   if constexpr (ZERO) {
     for (int r = r0; r < r1; ++r) {
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
       if constexpr (MULTI) pload<V>(pb + ro, pv);
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = (MULTI ? tab[pv[k] * kTabStride + 9] : om) * fv[k];
-      store_masked<T, V, NT>(ob + ro, o, cl, N);
+      store_masked<T, V, NT>(ob + ro, o, cl, W);
     }
   } else {
     Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
         const T omk = MULTI ? tab[p1.a[k + 1] + 9] : om;
         o[k] = omk * (fx[k] - acc) + w1.a[k + 1];
       }
-      store_masked<T, V, NT>(ob + rowo(r) + V * lane, o, cl, N);
+      store_masked<T, V, NT>(ob + rowo(r) + V * lane, o, cl, W);
       w0 = w1;
       w1 = w2;
       nx = nn;
@@ -387,10 +390,10 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N, Nc = g.Nc;
+  const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
   const int c0 = 1 + id.s * F::SW;
   const int I0 = 1 + id.t * (g.rb / 2);
-  const int I1 = min(I0 + g.rb / 2, Nc - 1);
+  const int I1 = min(I0 + g.rb / 2, Hc - 1);
   const int cl = c0 + V * lane;
   T ks[9], rs[9];
   T om = 0;
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
 #pragma unroll
   for (int j = 0; j < V + 3; ++j) {
     const int c = cl + j - 1;
-    cin[j] = c >= 1 && c <= N - 2;
+    cin[j] = c >= 1 && c <= W - 2;
   }
   const long long poff = F::OFF + c0;
   const long long boff = (long long)id.b * g.bs + poff;
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   const int bc0 = (c0 + 1) / 2;  // coarse column of lane 0's first output
   T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
   const int Jl = bc0 + Q * lane;
-  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, H) + 1) * ld; };
 
   // a window row: the field K acts on (u, or v = omd*f in ZERO mode), the f row, pattern offsets
   struct RawW {
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     if constexpr (MULTI) w.p = finish(r.p);
     w.f = finish(r.f);
     if constexpr (ZERO) {
-      const bool rin = y >= 1 && y <= N - 2;
+      const bool rin = y >= 1 && y <= H - 2;
 #pragma unroll
       for (int j = 0; j < V + 3; ++j) {
         const T omj = MULTI ? tab[w.p.a[j] + 9] : om;
@@ -461,12 +464,12 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   };
   auto store_v = [&](int y, const WRow& w) {
     if constexpr (ZERO) {
-      const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Nc - 1) && y <= N - 2;
+      const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
       if (own) {
         T o[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) o[k] = w.u.a[k + 1];
-        store_masked<T, V, NT>(vb + rowo(y) + V * lane, o, cl, N);
+        store_masked<T, V, NT>(vb + rowo(y) + V * lane, o, cl, W);
       }
     }
   };
@@ -525,12 +528,12 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
       o[q] = w0 * acc;
     }
     T* cp = cb + (long long)(I + 1) * g.ldc;
-    if (Jl + Q - 1 <= Nc - 2) {
+    if (Jl + Q - 1 <= Wc - 2) {
       vstore<T, Q, NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (Jl + q <= Nc - 2) cp[q] = o[q];
+        if (Jl + q <= Wc - 2) cp[q] = o[q];
     }
 #pragma unroll
     for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
@@ -643,10 +646,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N, Nc = g.Nc;
+  const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
   const int c0 = 1 + id.s * F::SW;
   const int I0 = 1 + id.t * (g.rb / 2);
-  const int I1 = min(I0 + g.rb / 2, Nc - 1);
+  const int I1 = min(I0 + g.rb / 2, Hc - 1);
   const int cl = c0 + V * lane;
   T ks[9], rs[9];
   T om = 0;
@@ -665,11 +668,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
 #pragma unroll
   for (int j = 0; j < V + 3; ++j) {
     const int c = cl + j - 1;
-    cin[j] = c >= 1 && c <= N - 2;
+    cin[j] = c >= 1 && c <= W - 2;
   }
   const int ce1 = L0 ? c0 - 1 : c0 + F::SW;  // centre column of edge sweep 1
-  const bool e1in = ce1 >= 1 && ce1 <= N - 2;
-  const bool e2in = c0 + F::SW + 1 <= N - 2;  // edge sweep 2 (lane 63): column c0+SW+1
+  const bool e1in = ce1 >= 1 && ce1 <= W - 2;
+  const bool e2in = c0 + F::SW + 1 <= W - 2;  // edge sweep 2 (lane 63): column c0+SW+1
   const long long poff = F::OFF + c0;
   const long long boff = (long long)id.b * g.bs + poff;
   const T* __restrict__ ub = g.u + boff;
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
   const int bc0 = (c0 + 1) / 2;
   T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
   const int Jl = bc0 + Q * lane;
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), N) + 1) * ld; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld; };
 
   struct RawS {
     XRaw<T, V> u;
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
   // u' row y (window columns L..RR) from input rows y-1, y, y+1 (a, b, c); boundary rows/cols keep u
   auto usweep = [&](const S& a, const S& b, const S& c, int y) {
     Row<T, V> o;
-    const bool rin = y >= 1 && y <= N - 2;
+    const bool rin = y >= 1 && y <= H - 2;
     T own[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -776,12 +779,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
     return o;
   };
   auto store_u = [&](int y, const Row<T, V>& w) {
-    const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Nc - 1) && y <= N - 2;
+    const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
     if (own) {
       T o[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = w.a[k + 1];
-      store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, N);
+      store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, W);
     }
   };
   const int ya = 2 * I0 - 1;  // first residual row
@@ -845,12 +848,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
     for (int q = 0; q < Q; ++q) o[q] = w0 * acc[q];
     racc(acc, r, X4.p.w, 0, true);
     T* cp = cb + (long long)(I + 1) * g.ldc;
-    if (Jl + Q - 1 <= Nc - 2) {
+    if (Jl + Q - 1 <= Wc - 2) {
       vstore<T, Q, NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (Jl + q <= Nc - 2) cp[q] = o[q];
+        if (Jl + q <= Wc - 2) cp[q] = o[q];
     }
     Uc = U1;
     Un = U2;
@@ -955,10 +958,10 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N, Nc = g.Nc;
+  const int H = g.H, Hc = g.Hc, W = g.W;
   const int c0 = 1 + id.s * F::SW;
   const int r0 = 1 + id.t * g.rb;  // odd
-  const int r1 = min(r0 + g.rb, N - 1);
+  const int r1 = min(r0 + g.rb, H - 1);
   const int cl = c0 + V * lane;
   T ks[9], ps[9];
   T om = 0;
@@ -982,8 +985,8 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const long long pcoff = F::OFF + bc0;
   const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + pcoff;
   const uint8_t* __restrict__ pcb = MULTI ? g.pidc + pcoff : nullptr;
-  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
-  auto crowo = [&](int a) -> long long { return (long long)(min(a, Nc) + 1) * ldc; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, H) + 1) * ld; };
+  auto crowo = [&](int a) -> long long { return (long long)(min(a, Hc) + 1) * ldc; };
 
   auto rc = [&](int a) { return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane); };
   auto ru = [&](int y) { return raw_row<T, V>(ub + rowo(y), lane); };
@@ -1014,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = b.a[k + 1];
     }
-    store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, N);
+    store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, W);
   };
 
   // window rows r0-1 (even, coarse a0) and r0 (odd, coarse a0, a0+1)
@@ -1086,10 +1089,10 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
   const int lane = lane_id();
-  const int N = g.N;
+  const int H = g.H, W = g.W;
   const int c0 = 1 + id.s * F::SW;
-  const int r0 = 1 + id.t * g.rb;
-  const int r1 = min(r0 + g.rb, N - 1);
+  const int r0 = g.rlo + id.t * g.rb;
+  const int r1 = min(r0 + g.rb, g.rhi);
   const int cl = c0 + V * lane;
   T ks[9];
   if constexpr (!MULTI) {
@@ -1102,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
   const T* __restrict__ fb = g.f + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
   const int ld = g.ld;
-  auto rowo = [&](int r) -> long long { return (long long)(min(r, N) + 1) * ld; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(r, H) + 1) * ld; };
   Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
   Row<T, V> w1 = finish(raw_row<T, V>(ub + rowo(r0), lane));
   RawRow<T, V> nx = raw_row<T, V>(ub + rowo(r0 + 1), lane);
@@ -1125,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T rr = fv[k] - kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
-      if (cl + k <= N - 2) s += (double)rr * (double)rr;
+      if (cl + k <= W - 2) s += (double)rr * (double)rr;
     }
     w0 = w1;
     w1 = w2;
@@ -1141,42 +1144,41 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
-// pack / unpack between contiguous [B,1,N,N] and the framed layout
+// pack / unpack between contiguous [B,1,H,W] and the framed layout
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_mg_pack(const T* __restrict__ src, T* __restrict__ dst,
                                                  const T* __restrict__ geo, long long geo_bs,
-                                                 const T* __restrict__ bc, long long bc_bs, int N, int ld,
+                                                 const T* __restrict__ bc, long long bc_bs, int H, int W, int ld,
                                                  long long bs) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), r = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
-  if (r >= N || c >= N) return;
-  const long long i = (long long)r * N + c;
-  const T v = src[(long long)b * N * N + i];
-  const T gv = geo ? geo[b * geo_bs + i] : T((r > 0 && r < N - 1 && c > 0 && c < N - 1) ? 1 : 0);
+  if (r >= H || c >= W) return;
+  const long long i = (long long)r * W + c;
+  const T v = src[(long long)b * H * W + i];
+  const T gv = geo ? geo[b * geo_bs + i] : T((r > 0 && r < H - 1 && c > 0 && c < W - 1) ? 1 : 0);
   const T bv = bc ? bc[b * bc_bs + i] : T(0);
   dst[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c] = v * gv + bv;
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_mg_unpack(const T* __restrict__ src, T* __restrict__ dst, int N, int ld,
-                                                   long long bs) {
+__global__ __launch_bounds__(256) void k_mg_unpack(const T* __restrict__ src, T* __restrict__ dst, int H, int W,
+                                                   int ld, long long bs) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), r = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
-  if (r >= N || c >= N) return;
-  dst[(long long)b * N * N + (long long)r * N + c] = src[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c];
+  if (r >= H || c >= W) return;
+  dst[(long long)b * H * W + (long long)r * W + c] = src[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c];
 }
 
 }  // namespace fea
 
 using namespace fea;
 
-static inline bool mg_n_ok(int N) {
-  if (N < 3 || N > (1 << 20) + 1) return false;
-  const int n = N - 1;
-  return (n & (n - 1)) == 0;
-}
+// Grid sizes: H, W >= 3; the intergrid kernels additionally need odd H and W (coarse (H+1)/2).
+static inline bool mg_dim_ok(int n) { return n >= 3 && n <= (1 << 20) + 1; }
+static inline bool mg_dims_ok(int H, int W) { return mg_dim_ok(H) && mg_dim_ok(W); }
+static inline bool mg_odd(int H, int W) { return (H & 1) && (W & 1); }
 
-// Rows per wave task: the largest even count (<= kRB) that still gives >= kTargetWaves waves,
-// so small levels are spread over the chip instead of being marched row by row by a few waves.
+// Rows per wave task: the largest even count (<= kRB) that still gives >= target waves, so small
+// levels are spread over the chip instead of being marched row by row by a few waves.
 // (tuning knobs are read at every launch so one process can A/B them; graphs capture the choice)
 static int target_waves() {
   const char* e = getenv("FEANET_TARGET_WAVES");  // default 2048 = 8 waves per CU
@@ -1197,184 +1199,220 @@ static long long nt_bytes() {
 }
 
 template <typename T>
-static MgArgs<T> mg_args(int N, int ld, long long bs, int B) {
+static MgArgs<T> mg_args(int H, int W, int ld, long long bs, int B) {
   MgArgs<T> g{};
   g.nt = (long long)B * bs * (long long)sizeof(T) > nt_bytes();
-  g.N = N;
+  g.H = H;
+  g.W = W;
   g.ld = ld;
   g.bs = bs;
-  g.nstrips = mg_nstrips<T>(N);
-  g.rb = pick_rb(B, g.nstrips, N - 2);
-  g.ntr = div_up(N - 2, g.rb);
+  g.nstrips = mg_nstrips<T>(W);
+  g.rb = pick_rb(B, g.nstrips, H - 2);
+  g.ntr = div_up(H - 2, g.rb);
+  g.rlo = 1;
+  g.rhi = H - 1;
   return g;
 }
 
 template <typename T>
-static inline bool layout_ok(int N, int ld, long long bs) {
-  return mg_n_ok(N) && ld >= mg_ld<T>(N) && ld % Frame<T>::A == 0 && bs >= (long long)(N + 2) * ld;
+static inline bool layout_ok(int H, int W, int ld, long long bs) {
+  return mg_dims_ok(H, W) && ld >= mg_ld<T>(W) && ld % Frame<T>::A == 0 && bs >= (long long)(H + 2) * ld;
+}
+
+// coarse grid of an intergrid kernel: (H+1)/2 x (W+1)/2 with its own framed layout
+template <typename T>
+static inline bool coarse_ok(int H, int W, int ldc, long long bsc) {
+  if (!mg_odd(H, W)) return false;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  return Hc >= 3 && Wc >= 3 && ldc >= mg_ld<T>(Wc) && ldc % Frame<T>::A == 0 && bsc >= (long long)(Hc + 2) * ldc;
 }
 
 static inline dim3 mg_grid(int B, int ntr, int nstrips) {
   return dim3((unsigned)(B * ntr * div_up(nstrips, kWaves)));
 }
 
-extern "C" int fea_abi_version(void) { return 1; }
+extern "C" int fea_abi_version(void) { return 2; }
 
-extern "C" int fea_mg_layout(int N, int elem_size, int* ld, long long* bstride) {
-  if (!mg_n_ok(N) || !ld || !bstride) return FEA_EINVAL;
+extern "C" int fea_mg_layout(int H, int W, int elem_size, int* ld, long long* bstride) {
+  if (!mg_dims_ok(H, W) || !ld || !bstride) return FEA_EINVAL;
   if (elem_size == 8) {
-    *ld = mg_ld<double>(N);
-    *bstride = mg_bstride<double>(N);
+    *ld = mg_ld<double>(W);
+    *bstride = mg_bstride<double>(H, W);
   } else if (elem_size == 4) {
-    *ld = mg_ld<float>(N);
-    *bstride = mg_bstride<float>(N);
+    *ld = mg_ld<float>(W);
+    *bstride = mg_bstride<float>(H, W);
   } else {
     return FEA_EINVAL;
   }
   return 0;
 }
 
-extern "C" size_t fea_norm_workspace_bytes(int B, int N) {
-  if (B <= 0 || N <= 0) return 0;
+extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
   // generic: one partial per 64x4 block; framed: one per (strip, row task) at the fp32 strip width
-  const long long gen = (long long)div_up(N, 64) * div_up(N, 4);
-  const long long frm = (long long)div_up(N, 64) * div_up(N, kRB);
+  const long long gen = (long long)div_up(W, 64) * div_up(H, 4);
+  const long long frm = (long long)div_up(W, 64) * div_up(H, 2);
   return (size_t)B * (size_t)std::max(gen, frm) * sizeof(double);
 }
 
+#define FEA_NT_LAUNCH(K, TARGS)                                   \
+  {                                                               \
+    if (g.nt) K<TARGS, true><<<grid, 256, 0, s>>>(g);             \
+    else K<TARGS, false><<<grid, 256, 0, s>>>(g);                 \
+  }
+
 #define FEA_MG_API(SUF, T)                                                                                   \
   extern "C" int fea_mg_pack_##SUF(const T* src, T* dst, const T* geo, long long geo_bs, const T* bc,         \
-                                   long long bc_bs, int B, int N, int ld, long long bs, void* stream) {       \
-    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                   \
-    k_mg_pack<T><<<dim3(div_up(N, 64), div_up(N, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, geo, geo_bs, \
-                                                                                       bc, bc_bs, N, ld, bs); \
+                                   long long bc_bs, int B, int H, int W, int ld, long long bs, void* stream) { \
+    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;                \
+    k_mg_pack<T><<<dim3(div_up(W, 64), div_up(H, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, geo, geo_bs, \
+                                                                                       bc, bc_bs, H, W, ld, bs); \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
-  extern "C" int fea_mg_unpack_##SUF(const T* src, T* dst, int B, int N, int ld, long long bs, void* stream) { \
-    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                   \
-    k_mg_unpack<T><<<dim3(div_up(N, 64), div_up(N, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, N, ld,  \
+  extern "C" int fea_mg_unpack_##SUF(const T* src, T* dst, int B, int H, int W, int ld, long long bs,         \
+                                     void* stream) {                                                         \
+    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;                \
+    k_mg_unpack<T><<<dim3(div_up(W, 64), div_up(H, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, H, W, ld, \
                                                                                          bs);                \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_sweep_##SUF(const T* u, const T* f, T* out, const uint8_t* pid, const T* ktab,         \
-                                    const T* omd, int ntab, int B, int N, int ld, long long bs, void* stream) { \
-    if (!f || !out || !ktab || !omd || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                 \
+                                    const T* omd, int ntab, int B, int H, int W, int ld, long long bs,         \
+                                    void* stream) {                                                          \
+    if (!f || !out || !ktab || !omd || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;              \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || out == u) return FEA_EINVAL;             \
-    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;                   \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (!u) {                                                                                                \
-      if (multi) { if (g.nt) k_mg_sweep<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                          \
-      else { if (g.nt) k_mg_sweep<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                               \
+      if (multi) FEA_NT_LAUNCH(k_mg_sweep, T COMMA true COMMA true)                                          \
+      else FEA_NT_LAUNCH(k_mg_sweep, T COMMA false COMMA true)                                               \
     } else {                                                                                                 \
-      if (multi) { if (g.nt) k_mg_sweep<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                         \
-      else { if (g.nt) k_mg_sweep<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                              \
+      if (multi) FEA_NT_LAUNCH(k_mg_sweep, T COMMA true COMMA false)                                         \
+      else FEA_NT_LAUNCH(k_mg_sweep, T COMMA false COMMA false)                                              \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_residual_restrict_##SUF(const T* u, const T* f, T* v_out, T* fc, const uint8_t* pid, \
                                                 const T* ktab, const T* omd, int ntab, const T* rtab,          \
-                                                int nrtab, T w0, int B, int N, int ld, long long bs, int ldc,  \
-                                                long long bsc, void* stream) {                               \
-    if (!f || !fc || !ktab || !rtab || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;                  \
-    const int Nc = (N + 1) / 2;                                                                              \
-    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+                                                int nrtab, T w0, int B, int H, int W, int ld, long long bs,    \
+                                                int ldc, long long bsc, void* stream) {                        \
+    if (!f || !fc || !ktab || !rtab || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;               \
+    if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
     if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;                                                      \
     if (!u && (!v_out || !omd)) return FEA_EINVAL;                                                           \
-    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.out = fc; g.out2 = v_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
-    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;                           \
-    g.ntr = div_up(Nc - 2, g.rb / 2);                                                                        \
+    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
+    g.bsc = bsc;                                                                                             \
+    g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
     if (!u) {                                                                                                \
-      if (multi) { if (g.nt) k_mg_resid_restrict<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                 \
-      else { if (g.nt) k_mg_resid_restrict<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                      \
+      if (multi) FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA true COMMA true)                                 \
+      else FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA false COMMA true)                                      \
     } else {                                                                                                 \
-      if (multi) { if (g.nt) k_mg_resid_restrict<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                \
-      else { if (g.nt) k_mg_resid_restrict<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_resid_restrict<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                     \
+      if (multi) FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA true COMMA false)                                \
+      else FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA false COMMA false)                                     \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_sweep_restrict_##SUF(const T* u, const T* f, T* u_out, T* fc, const uint8_t* pid,       \
                                              const T* ktab, const T* omd, int ntab, const T* rtab, int nrtab,    \
-                                             T w0, int B, int N, int ld, long long bs, int ldc, long long bsc,  \
-                                             void* stream) {                                                   \
-    if (!u || !f || !u_out || !fc || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(N, ld, bs) || u_out == u) \
+                                             T w0, int B, int H, int W, int ld, long long bs, int ldc,          \
+                                             long long bsc, void* stream) {                                    \
+    if (!u || !f || !u_out || !fc || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(H, W, ld, bs) ||       \
+        u_out == u)                                                                                          \
       return FEA_EINVAL;                                                                                     \
-    const int Nc = (N + 1) / 2;                                                                              \
-    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+    if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || (nrtab != ntab && nrtab != 1))          \
       return FEA_EINVAL;                                                                                     \
     if (ntab > 1 && nrtab == 1) return FEA_EINVAL;                                                           \
-    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                  \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
-    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;                           \
-    g.ntr = div_up(Nc - 2, g.rb / 2);                                                                        \
+    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
+    g.bsc = bsc;                                                                                             \
+    g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (ntab > 1) { if (g.nt) k_mg_sweep_restrict<T, true, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep_restrict<T, true, false><<<grid, 256, 0, s>>>(g); }                                      \
-    else { if (g.nt) k_mg_sweep_restrict<T, false, true><<<grid, 256, 0, s>>>(g); else k_mg_sweep_restrict<T, false, false><<<grid, 256, 0, s>>>(g); }                                              \
+    if (ntab > 1) FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA true)                                           \
+    else FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA false)                                                   \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \
                               const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab,      \
-                              int nptab, T w1, int B, int N, int ld, long long bs, int ldc, long long bsc,   \
-                              void* stream, bool sweep) {                                                    \
-    if (!u || !ec || !out || !ptab || B <= 0 || !layout_ok<T>(N, ld, bs) || out == u) return FEA_EINVAL;      \
-    const int Nc = (N + 1) / 2;                                                                              \
-    if (Nc < 3 || ldc < mg_ld<T>(Nc) || ldc % Frame<T>::A || bsc < (long long)(Nc + 2) * ldc) return FEA_EINVAL; \
+                              int nptab, T w1, int B, int H, int W, int ld, long long bs, int ldc,           \
+                              long long bsc, void* stream, bool sweep) {                                     \
+    if (!u || !ec || !out || !ptab || B <= 0 || !layout_ok<T>(H, W, ld, bs) || out == u) return FEA_EINVAL;   \
+    if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (nptab < 1 || nptab > FEA_MAX_PATTERNS || (nptab > 1 && !pidc)) return FEA_EINVAL;                    \
     if (sweep && (!f || !ktab || !omd || ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)))          \
       return FEA_EINVAL;                                                                                     \
     const bool multi = nptab > 1 || (sweep && ntab > 1);                                                     \
     if (multi && ((sweep && (!pid || ntab == 1)) || !pidc || nptab == 1)) return FEA_EINVAL;                 \
-    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.ec = ec; g.f = f; g.out = out; g.pid = pid; g.pidc = pidc; g.ktab = ktab; g.omd = omd;         \
-    g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Nc = Nc; g.ldc = ldc; g.bsc = bsc;            \
+    g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2;          \
+    g.ldc = ldc; g.bsc = bsc;                                                                                \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (sweep) {                                                                                             \
-      if (multi) { if (g.nt) k_mg_prolong<T, true, true, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, true, true, false><<<grid, 256, 0, s>>>(g); }                                        \
-      else { if (g.nt) k_mg_prolong<T, false, true, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, false, true, false><<<grid, 256, 0, s>>>(g); }                                             \
+      if (multi) FEA_NT_LAUNCH(k_mg_prolong, T COMMA true COMMA true)                                        \
+      else FEA_NT_LAUNCH(k_mg_prolong, T COMMA false COMMA true)                                             \
     } else {                                                                                                 \
-      if (multi) { if (g.nt) k_mg_prolong<T, true, false, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, true, false, false><<<grid, 256, 0, s>>>(g); }                                       \
-      else { if (g.nt) k_mg_prolong<T, false, false, true><<<grid, 256, 0, s>>>(g); else k_mg_prolong<T, false, false, false><<<grid, 256, 0, s>>>(g); }                                            \
+      if (multi) FEA_NT_LAUNCH(k_mg_prolong, T COMMA true COMMA false)                                       \
+      else FEA_NT_LAUNCH(k_mg_prolong, T COMMA false COMMA false)                                            \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_prolong_sweep_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,  \
                                             const uint8_t* pidc, const T* ktab, const T* omd, int ntab,       \
-                                            const T* ptab, int nptab, T w1, int B, int N, int ld,            \
+                                            const T* ptab, int nptab, T w1, int B, int H, int W, int ld,     \
                                             long long bs, int ldc, long long bsc, void* stream) {             \
-    return mg_prolong_##SUF(u, ec, f, out, pid, pidc, ktab, omd, ntab, ptab, nptab, w1, B, N, ld, bs, ldc,   \
+    return mg_prolong_##SUF(u, ec, f, out, pid, pidc, ktab, omd, ntab, ptab, nptab, w1, B, H, W, ld, bs, ldc, \
                             bsc, stream, true);                                                              \
   }                                                                                                          \
   extern "C" int fea_mg_prolong_add_##SUF(const T* u, const T* ec, T* out, const uint8_t* pidc, const T* ptab, \
-                                          int nptab, T w1, int B, int N, int ld, long long bs, int ldc,       \
+                                          int nptab, T w1, int B, int H, int W, int ld, long long bs, int ldc, \
                                           long long bsc, void* stream) {                                     \
-    return mg_prolong_##SUF(u, ec, nullptr, out, nullptr, pidc, nullptr, nullptr, 0, ptab, nptab, w1, B, N,  \
-                            ld, bs, ldc, bsc, stream, false);                                                \
+    return mg_prolong_##SUF(u, ec, nullptr, out, nullptr, pidc, nullptr, nullptr, 0, ptab, nptab, w1, B, H,  \
+                            W, ld, bs, ldc, bsc, stream, false);                                             \
   }                                                                                                          \
   extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \
-                                            int ntab, double* out, double* ws, int B, int N, int ld,          \
-                                            long long bs, void* stream) {                                    \
-    if (!u || !f || !ktab || !out || !ws || B <= 0 || !layout_ok<T>(N, ld, bs)) return FEA_EINVAL;            \
+                                            int ntab, double* out, double* ws, int B, int H, int W, int ld,   \
+                                            long long bs, int rlo, int rhi, void* stream) {                  \
+    if (!u || !f || !ktab || !out || !ws || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;         \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
-    MgArgs<T> g = mg_args<T>(N, ld, bs, B);                                                                     \
+    if (rlo == 0 && rhi == 0) {                                                                              \
+      rlo = 1;                                                                                               \
+      rhi = H - 1;                                                                                           \
+    }                                                                                                        \
+    if (rlo < 1 || rhi > H - 1 || rhi < rlo) return FEA_EINVAL;                                              \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.pid = pid; g.ktab = ktab; g.ntab = ntab; g.part = ws;                                \
+    g.rlo = rlo; g.rhi = rhi;                                                                                \
+    g.rb = 2;                                                                                                \
+    while (g.rb < kRB && (long long)B * g.nstrips * div_up(rhi - rlo, g.rb * 2) >= target_waves()) g.rb *= 2; \
+    g.ntr = std::max(div_up(rhi - rlo, g.rb), 1);                                                            \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (ntab > 1) k_mg_resnorm<T, true><<<grid, 256, 0, s>>>(g);                                             \
-    else k_mg_resnorm<T, false><<<grid, 256, 0, s>>>(g);                                                     \
-    k_norm_final<<<B, 256, 0, s>>>(ws, (long long)g.ntr * g.nstrips, out);                               \
+    if (rhi == rlo) {                                                                                        \
+      hipMemsetAsync(ws, 0, sizeof(double) * (size_t)B * g.nstrips, s);                                      \
+      g.ntr = 1;                                                                                             \
+    } else if (ntab > 1) {                                                                                   \
+      k_mg_resnorm<T, true><<<grid, 256, 0, s>>>(g);                                                         \
+    } else {                                                                                                 \
+      k_mg_resnorm<T, false><<<grid, 256, 0, s>>>(g);                                                        \
+    }                                                                                                        \
+    k_norm_final<<<B, 256, 0, s>>>(ws, (long long)g.ntr * g.nstrips, out);                                   \
     FEA_LAUNCH_CHECK();                                                                                      \
   }
 
+#define COMMA ,
 FEA_MG_API(f32, float)
 FEA_MG_API(f64, double)

@@ -11,7 +11,7 @@ import torch  # noqa: F401  (must precede the CDLL load)
 
 from .build import LIB
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -28,21 +28,22 @@ _SIGS = {
     "restrict": [P, I, P, P, P, I, "S", I, I, I, P],
     "prolong": [P, I, P, P, P, P, I, "S", I, I, I, P],
     "residual_norm": [P, P, P, P, I, P, P, I, I, I, P],
-    "mg_pack": [P, P, P, LL, P, LL, I, I, I, LL, P],
-    "mg_unpack": [P, P, I, I, I, LL, P],
-    "mg_sweep": [P, P, P, P, P, P, I, I, I, I, LL, P],
-    "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
-    "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
-    "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, LL, I, LL, P],
-    "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, LL, I, LL, P],
-    "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, LL, P],
-    "mg_coarse_tail": [P, P, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
+    # framed level ops: (..., B, H, W, ld, bstride[, ldc, bstridec], stream)
+    "mg_pack": [P, P, P, LL, P, LL, I, I, I, I, LL, P],
+    "mg_unpack": [P, P, I, I, I, I, LL, P],
+    "mg_sweep": [P, P, P, P, P, P, I, I, I, I, I, LL, P],
+    "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, I, LL, I, I, P],
+    "mg_coarse_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
 }
 _EXTRA = {
     "fea_abi_version": ([], I),
-    "fea_mg_layout": ([I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
-    "fea_norm_workspace_bytes": ([I, I], ctypes.c_size_t),
-    "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I], ctypes.c_size_t),
+    "fea_mg_layout": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
+    "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
+    "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
 }
 
 _lib = None
@@ -91,20 +92,21 @@ def call(name, dtype, *args):
         raise RuntimeError(f"feanet_amd: fea_{name}_{suf} failed ({what})")
 
 
-def mg_layout(N, elem_size):
+def mg_layout(H, W, elem_size):
+    """(ld, bstride) of the framed layout of an H x W grid."""
     ld = I()
     bs = LL()
-    if lib().fea_mg_layout(N, elem_size, ctypes.byref(ld), ctypes.byref(bs)) != 0:
-        raise ValueError(f"feanet_amd: unsupported level size N={N} (need N = 2^k + 1 >= 5)")
+    if lib().fea_mg_layout(H, W, elem_size, ctypes.byref(ld), ctypes.byref(bs)) != 0:
+        raise ValueError(f"feanet_amd: unsupported level size {H} x {W} (need H, W >= 3)")
     return ld.value, bs.value
 
 
 TAIL_LDS_LIMIT = 160 * 1024 - 1024
 
 
-def coarse_tail_lds_bytes(Nt, nlev, elem_size, multi):
-    return int(lib().fea_mg_coarse_tail_lds_bytes(Nt, nlev, elem_size, int(bool(multi))))
+def coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, multi):
+    return int(lib().fea_mg_coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, int(bool(multi))))
 
 
-def norm_workspace_bytes(B, N):
-    return int(lib().fea_norm_workspace_bytes(B, N))
+def norm_workspace_bytes(B, H, W):
+    return int(lib().fea_norm_workspace_bytes(B, H, W))

@@ -187,7 +187,7 @@ def residual_norm(u, f=None, ktab=None, pid=None):
         f = _field(f, "f", u.dtype)
         tab = _table(ktab, u.dtype, u.device)
         pid = _pid(pid, H, W, u.device)
-    ws = torch.empty(max(1, _lib.norm_workspace_bytes(B, max(H, W)) // 8), dtype=torch.float64, device=u.device)
+    ws = torch.empty(max(1, _lib.norm_workspace_bytes(B, H, W) // 8), dtype=torch.float64, device=u.device)
     out = torch.empty(B, dtype=torch.float64, device=u.device)
     _lib.call("residual_norm", u.dtype, u.data_ptr(), _ptr(f), _ptr(pid) if f is not None else None,
               _ptr(tab), 0 if tab is None else tab.shape[0], out.data_ptr(), ws.data_ptr(), B, H, W, _stream(u))

@@ -26,11 +26,14 @@ from .schedule import vcycle_schedule
 
 
 class _Level:
-    def __init__(self, n, B, dtype, device, pid_np=None):
-        self.n = n
-        self.N = n + 1
+    """Framed buffers of one level: H x W nodes (H = rows, W = columns)."""
+
+    def __init__(self, m, n, B, dtype, device, pid_np=None):
+        self.m, self.n = m, n
+        self.H, self.W = m + 1, n + 1
+        self.N = self.W
         esz = 4 if dtype == torch.float32 else 8
-        self.ld, self.bs = _lib.mg_layout(self.N, esz)
+        self.ld, self.bs = _lib.mg_layout(self.H, self.W, esz)
         self.B = B
         self.dtype = dtype
         self.device = device
@@ -42,8 +45,8 @@ class _Level:
         self.pid = None
         if pid_np is not None:
             off = 128 // esz - 1
-            p = np.zeros((self.N + 2, self.ld), np.uint8)
-            p[1:self.N + 1, off:off + self.N] = pid_np
+            p = np.zeros((self.H + 2, self.ld), np.uint8)
+            p[1:self.H + 1, off:off + self.W] = pid_np
             self.pid = torch.from_numpy(p.reshape(-1)).to(device)
             self.pid = torch.cat([self.pid, torch.zeros(256, dtype=torch.uint8, device=device)])
 
@@ -55,9 +58,12 @@ class _Level:
         return getattr(self, name)
 
     def view(self, t):
-        """[B, N, N] view of the interior+boundary nodes of a framed buffer (plumbing / tests)."""
+        """[B, H, W] view of the interior+boundary nodes of a framed buffer (plumbing / tests)."""
         off = 128 // t.element_size() - 1
-        return t[:self.B * self.bs].view(self.B, self.N + 2, self.ld)[:, 1:self.N + 1, off:off + self.N]
+        return t[:self.B * self.bs].view(self.B, self.H + 2, self.ld)[:, 1:self.H + 1, off:off + self.W]
+
+    def geom(self):
+        return (self.B, self.H, self.W, self.ld, self.bs)
 
 
 class MultigridSolver:
@@ -65,7 +71,10 @@ class MultigridSolver:
 
     Args:
         n: fine-grid intervals per edge (N = n + 1 nodes), a power of two >= 2.
-        levels: number of levels L (default int(log2 n), the reference's choice; coarsest n/2^(L-1)).
+        rows: intervals in the row direction when the domain is a rectangle (Poisson only; default
+            n, the reference's square).  n and rows must be divisible by 2^(L-1).
+        levels: number of levels L (default int(log2 n), the reference's choice; coarsest n/2^(L-1);
+            for a rectangle, the most levels whose coarsest grid has >= 2 intervals each way).
         problem: "poisson" (MeshSquare, one stencil) or "interface" (MeshCenterInterface, 16
             stencils; `prop` coefficients, `shape` 0 circle / 1 rectangle inclusion).
         dtype: torch.float32 or torch.float64.  batch: number of right-hand sides B.
@@ -85,17 +94,27 @@ class MultigridSolver:
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
-                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True):
-        if n < 2 or (n & (n - 1)) != 0:
+                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None):
+        m = n if rows is None else int(rows)
+        if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
+        if m < 2 or n < 2:
+            raise ValueError(f"MultigridSolver: need >= 2 intervals each way (got {m} x {n})")
         if dtype not in (torch.float32, torch.float64):
             raise TypeError("MultigridSolver: dtype must be torch.float32 or torch.float64")
         self.device = torch.device(device if device is not None else "cuda")
         ops.require_hip(torch.empty(0, device=self.device), "solver device")
-        self.n = n
-        self.L = int(math.log2(n)) if levels is None else int(levels)
-        if self.L < 1 or (n >> (self.L - 1)) < 2:
-            raise ValueError(f"MultigridSolver: {self.L} levels do not fit n={n}")
+        self.n, self.m = n, m
+        if levels is None:
+            L = 1
+            while (n % (1 << L) == 0 and m % (1 << L) == 0 and (n >> L) >= 2 and (m >> L) >= 2):
+                L += 1
+            self.L = L if rows is not None else int(math.log2(n))
+        else:
+            self.L = int(levels)
+        s_ = 1 << (self.L - 1)
+        if self.L < 1 or n % s_ or m % s_ or n // s_ < 2 or m // s_ < 2:
+            raise ValueError(f"MultigridSolver: {self.L} levels do not fit a {m} x {n} grid")
         self.dtype = dtype
         self.B = int(batch)
         self.omega = omega
@@ -109,6 +128,8 @@ class MultigridSolver:
         multi = problem == "interface"
         if problem not in ("poisson", "interface"):
             raise ValueError(f"MultigridSolver: unknown problem {problem!r}")
+        if multi and m != n:
+            raise ValueError("MultigridSolver: the two-material problem is defined on the square only")
         ktab = ms.stencil_table(prop if multi else None)
         self.ntab = ktab.shape[0]
         lin = ms.linear_transfer_kernel() / np.float32(4.0)
@@ -131,16 +152,17 @@ class MultigridSolver:
         self.ptab = torch.from_numpy(np.ascontiguousarray(P).reshape(-1, 9).astype(npdt)).to(dev)
         self.levels = []
         for l in range(self.L):
-            nl = n >> l
+            nl, ml = n >> l, m >> l
             pid = ms.interface_pattern_map(nl + 1, shape, size) if multi else None
-            self.levels.append(_Level(nl, self.B, dtype, dev, pid))
+            self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid))
         self.fine_pid = (torch.from_numpy(ms.interface_pattern_map(n + 1, shape, size)).to(dev) if multi else None)
         self.tail_from = None
         if coarse_tail:
             esz = 4 if dtype == torch.float32 else 8
             for l in range(1, self.L):
-                Nl = self.levels[l].N
-                if Nl <= 65 and _lib.coarse_tail_lds_bytes(Nl, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT:
+                Lv = self.levels[l]
+                if (Lv.H <= 65 and Lv.W <= 65
+                        and 0 < _lib.coarse_tail_lds_bytes(Lv.H, Lv.W, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT):
                     self.tail_from = l
                     break
         if self.tail_from is not None and multi:
@@ -149,7 +171,7 @@ class MultigridSolver:
             self.tail_pid = torch.from_numpy(np.concatenate(maps)).to(dev)
         else:
             self.tail_pid = None
-        self.ws = torch.zeros(max(1, _lib.norm_workspace_bytes(self.B, n + 1) // 8), dtype=torch.float64,
+        self.ws = torch.zeros(max(1, _lib.norm_workspace_bytes(self.B, m + 1, n + 1) // 8), dtype=torch.float64,
                               device=dev)
         self.norm_out = torch.zeros(self.B, dtype=torch.float64, device=dev)
         self._state = "a"
@@ -163,14 +185,23 @@ class MultigridSolver:
     def N(self):
         return self.n + 1
 
+    @property
+    def H(self):
+        return self.m + 1
+
+    @property
+    def W(self):
+        return self.n + 1
+
     def _check_field(self, x, name):
         ops.require_hip(x, name)
         x = x.to(self.dtype)
-        if x.numel() == self.N * self.N:
-            x = x.reshape(1, 1, self.N, self.N).expand(self.B, 1, self.N, self.N)
-        if tuple(x.shape[-2:]) != (self.N, self.N) or x.numel() != self.B * self.N * self.N:
-            raise ValueError(f"MultigridSolver: {name} must be [{self.B}, 1, {self.N}, {self.N}]")
-        return x.reshape(self.B, 1, self.N, self.N).contiguous()
+        H, W = self.H, self.W
+        if x.numel() == H * W:
+            x = x.reshape(1, 1, H, W).expand(self.B, 1, H, W)
+        if tuple(x.shape[-2:]) != (H, W) or x.numel() != self.B * H * W:
+            raise ValueError(f"MultigridSolver: {name} must be [{self.B}, 1, {H}, {W}]")
+        return x.reshape(self.B, 1, H, W).contiguous()
 
     def set_rhs(self, f=None, F=None):
         """Set the assembled right-hand side f (= FNet(F), the `forcing_term` of the reference) or
@@ -204,32 +235,32 @@ class MultigridSolver:
         gp, gs = (None, 0)
         bp, bs = (None, 0)
         if bc is not None:
-            bp, bs = bc.data_ptr(), self.N * self.N
+            bp, bs = bc.data_ptr(), self.H * self.W
         if reset:
-            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), gp, gs, bp, bs, self.B, self.N, Lv.ld,
-                      Lv.bs, ops._stream(x))
+            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), gp, gs, bp, bs, *Lv.geom(),
+                      ops._stream(x))
         else:  # raw copy: geometry = all ones
             ones = torch.ones_like(x)
-            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), ones.data_ptr(), self.N * self.N,
-                      None, 0, self.B, self.N, Lv.ld, Lv.bs, ops._stream(x))
+            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), ones.data_ptr(), self.H * self.W,
+                      None, 0, *Lv.geom(), ops._stream(x))
 
     def load(self, u0=None):
         """Set the fine-grid iterate (reset_boundary applied: u*geo + bc, jacobi.py:27-29)."""
         L0 = self.levels[0]
         bc = getattr(self, "_bc", None)
         if u0 is None:
-            u0 = torch.zeros((self.B, 1, self.N, self.N), dtype=self.dtype, device=self.device)
+            u0 = torch.zeros((self.B, 1, self.H, self.W), dtype=self.dtype, device=self.device)
         u0 = self._check_field(u0, "u0")
         self._pack(u0, L0.a, bc=bc)
         self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
         self._state = "a"
 
     def solution(self):
-        """Current fine iterate as a contiguous [B, 1, N, N] tensor."""
+        """Current fine iterate as a contiguous [B, 1, H, W] tensor."""
         L0 = self.levels[0]
-        out = torch.empty((self.B, 1, self.N, self.N), dtype=self.dtype, device=self.device)
-        _lib.call("mg_unpack", self.dtype, L0.buf(self._state).data_ptr(), out.data_ptr(), self.B, self.N, L0.ld,
-                  L0.bs, ops._stream(out))
+        out = torch.empty((self.B, 1, self.H, self.W), dtype=self.dtype, device=self.device)
+        _lib.call("mg_unpack", self.dtype, L0.buf(self._state).data_ptr(), out.data_ptr(), *L0.geom(),
+                  ops._stream(out))
         return out
 
     def residual_norm(self):
@@ -237,7 +268,7 @@ class MultigridSolver:
         L0 = self.levels[0]
         _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(),
                   None if L0.pid is None else L0.pid.data_ptr(), self.ktab.data_ptr(), self.ntab,
-                  self.norm_out.data_ptr(), self.ws.data_ptr(), self.B, self.N, L0.ld, L0.bs,
+                  self.norm_out.data_ptr(), self.ws.data_ptr(), *L0.geom(), 0, 0,
                   torch.cuda.current_stream(self.device).cuda_stream)
         return self.norm_out.clone()
 
@@ -261,7 +292,7 @@ class MultigridSolver:
             return None if name is None else self._ptr(l, name)
 
         def geom(l):
-            return (lv[l].B, lv[l].N, lv[l].ld, lv[l].bs)
+            return lv[l].geom()
 
         def cgeom(l):
             return (lv[l + 1].ld, lv[l + 1].bs)
@@ -286,7 +317,7 @@ class MultigridSolver:
                                                 self.w[1]) + geom(l) + cgeom(l)))
             elif kind == "coarse_tail":
                 t = l
-                plan.append(("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].N, self.L - t, lv[t].ld,
+                plan.append(("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
                                                 lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
                                                 kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
                                                 int(self.compat == "mm_interface_q2"), lv[t].B)))
@@ -357,10 +388,10 @@ class MultigridSolver:
         for name, args in self._plan(self._state)[0]:
             if name == "mg_coarse_tail":
                 continue
-            B, N = (args[-6:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",
-                                            "mg_sweep_restrict") else args[-4:-2])
-            nodes = B * (N - 2) ** 2
-            coarse = B * ((N + 1) // 2 - 2) ** 2
+            B, H, W = (args[-7:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",
+                                               "mg_sweep_restrict") else args[-5:-2])
+            nodes = B * (H - 2) * (W - 2)
+            coarse = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
             if name == "mg_sweep":
                 total += nodes * (esz * (3 if args[0] is not None else 2) + pb)
             elif name == "mg_residual_restrict":

@@ -54,10 +54,15 @@ def pattern_stencil(a, pattern, Ke=None):
     return k
 
 
+def _hw(N):
+    return (N, N) if np.isscalar(N) else tuple(N)
+
+
 def square_mesh(N):
-    """MeshSquare (FEANet/mesh.py:122-189): one pattern (all-background), every node pattern 0."""
+    """MeshSquare (FEANet/mesh.py:122-189): one pattern (all-background), every node pattern 0.
+    N: nodes per edge, or (H, W) for the rectangular extension used by the domain-decomposed path."""
     ktab = pattern_stencil(np.array([1.], np.float32), REF_PATTERNS[0])[None]
-    return ktab, np.zeros((N, N), np.uint8)
+    return ktab, np.zeros(_hw(N), np.uint8)
 
 
 def interface_mesh(N, prop=(1, 20), shape=0, size=2):
@@ -109,10 +114,11 @@ def interface_mesh(N, prop=(1, 20), shape=0, size=2):
 
 
 def square_geometry(N, dtype=np.float32):
-    """Geometry.square_geometry (FEANet/geo.py:13-30): 1 inside, 0 on the boundary; zero bc."""
-    geo = np.ones((N, N), dtype)
+    """Geometry.square_geometry (FEANet/geo.py:13-30): 1 inside, 0 on the boundary; zero bc.
+    N: nodes per edge or (H, W)."""
+    geo = np.ones(_hw(N), dtype)
     geo[0, :] = geo[-1, :] = geo[:, 0] = geo[:, -1] = 0
-    return geo, np.zeros((N, N), dtype)
+    return geo, np.zeros(_hw(N), dtype)
 
 
 def fnet_stencil(h):
@@ -271,15 +277,18 @@ def hnet(x, geo, weights):
 # A11-A14: V-cycles
 # ---------------------------------------------------------------------------
 class Level:
-    def __init__(self, n, problem="poisson", dtype=np.float32, prop=(1, 20), shape=0, omega=2. / 3.):
+    def __init__(self, n, problem="poisson", dtype=np.float32, prop=(1, 20), shape=0, omega=2. / 3., m=None):
         self.n = n
+        self.m = n if m is None else m
         self.N = n + 1
+        self.H, self.W = self.m + 1, n + 1
         self.dtype = dtype
         if problem == "poisson":
-            self.ktab, self.pid = square_mesh(self.N)
+            self.ktab, self.pid = square_mesh((self.H, self.W))
         else:
+            assert self.m == n, "two-material problem: square only"
             self.ktab, self.pid = interface_mesh(self.N, prop, shape)
-        self.geo, self.bc = square_geometry(self.N, dtype)
+        self.geo, self.bc = square_geometry((self.H, self.W), dtype)
         self.omega = omega
 
     def sweep(self, v, f):
@@ -301,10 +310,11 @@ class OracleMultigrid:
                MM_Interface_error.ipynb:141 (pre-smoothing applied to grids[0] at every depth)."""
 
     def __init__(self, n, problem="poisson", dtype=np.float32, levels=None, rtab=None, ptab=None,
-                 w=(1.0, 1.0), prop=(1, 20), shape=0):
+                 w=(1.0, 1.0), prop=(1, 20), shape=0, rows=None):
         self.n = n
-        self.L = int(np.log2(n)) if levels is None else levels
-        self.levels = [Level(n >> l, problem, dtype, prop, shape) for l in range(self.L)]
+        m = n if rows is None else rows
+        self.L = int(np.log2(min(n, m))) if levels is None else levels
+        self.levels = [Level(n >> l, problem, dtype, prop, shape, m=m >> l) for l in range(self.L)]
         lin = np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float32)
         nch = len(self.levels[0].ktab)
         self.rtab = (np.broadcast_to(lin / 4, (nch, 3, 3)) if rtab is None else np.asarray(rtab, np.float32))
@@ -327,7 +337,7 @@ class OracleMultigrid:
         for j in range(L - 1):
             r = fs[j] - lv[j].K(vs[j])
             fs[j + 1] = restrict(r, lv[j].pid, self.rtab, self.w[0])
-            z = np.zeros((B, lv[j + 1].N, lv[j + 1].N), self.dtype)
+            z = np.zeros((B, lv[j + 1].H, lv[j + 1].W), self.dtype)
             vs[j + 1] = lv[j + 1].sweep(z, fs[j + 1])
         vs[L - 1] = lv[L - 1].sweep(vs[L - 1], fs[L - 1])
         for j in range(L - 2, -1, -1):
@@ -363,7 +373,7 @@ class OracleMultigrid:
             if l < L - 1:
                 r = fs[l] - lv[l].K(vs[l])
                 fs[l + 1] = self._mm_restrict(r)
-                vs[l + 1] = np.zeros((B, lv[l + 1].N, lv[l + 1].N), dt)
+                vs[l + 1] = np.zeros((B, lv[l + 1].H, lv[l + 1].W), dt)
                 rec(l + 1)
                 up = bilinear_upsample(vs[l + 1])
                 vs[l] = vs[l] + (up * lv[l].geo + lv[l].bc)

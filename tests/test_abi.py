@@ -32,13 +32,14 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_queries():
     from feanet_amd import _lib
     assert _lib.lib().fea_abi_version() == _lib.ABI_VERSION
-    for N, esz in [(3, 8), (5, 8), (4097, 8), (1025, 4), (8193, 8)]:
-        ld, bs = _lib.mg_layout(N, esz)
+    for H, W, esz in [(3, 3, 8), (5, 5, 8), (4097, 4097, 8), (1025, 1025, 4), (8193, 8193, 8), (517, 4097, 8),
+                      (9, 100, 4)]:
+        ld, bs = _lib.mg_layout(H, W, esz)
         A = 128 // esz
-        assert ld % A == 0 and ld >= N + A and bs == (N + 2) * ld
+        assert ld % A == 0 and ld >= W + A and bs == (H + 2) * ld
     with pytest.raises(ValueError):
-        _lib.mg_layout(100, 8)       # not 2^k + 1
-    assert _lib.norm_workspace_bytes(2, 4097) >= 2 * 65 * 129 * 8
+        _lib.mg_layout(2, 100, 8)       # fewer than 3 rows
+    assert _lib.norm_workspace_bytes(2, 4097, 4097) >= 2 * 65 * 129 * 8
 
 
 def test_ops_refuse_cpu_tensors():

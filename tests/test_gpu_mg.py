@@ -31,12 +31,15 @@ def close(out, ref, T, what):
 class Frame:
     """A framed level (via the solver's level allocator) with numpy I/O for tests."""
 
-    def __init__(self, n, B, T, problem):
+    def __init__(self, n, B, T, problem, m=None):
         from feanet_amd.solver import _Level
         from feanet_amd import mesh_setup as ms
+        m = n if m is None else m
         self.N = n + 1
-        self.pid_np = ms.interface_pattern_map(self.N) if problem == "interface" else np.zeros((self.N, self.N), np.uint8)
-        self.L = _Level(n, B, T, torch.device("cuda"), self.pid_np if problem == "interface" else None)
+        self.H, self.W = m + 1, n + 1
+        self.pid_np = (ms.interface_pattern_map(self.N) if problem == "interface"
+                       else np.zeros((self.H, self.W), np.uint8))
+        self.L = _Level(m, n, B, T, torch.device("cuda"), self.pid_np if problem == "interface" else None)
         self.T = T
 
     def put(self, name, arr):
@@ -46,7 +49,7 @@ class Frame:
         return self.L.view(self.L.buf(name)).cpu().numpy()
 
     def args(self):
-        return (self.L.B, self.N, self.L.ld, self.L.bs)
+        return self.L.geom()
 
     def pid(self):
         return None if self.L.pid is None else self.L.pid.data_ptr()
@@ -69,8 +72,9 @@ def tables(problem, T, learned=False):
 
 
 def rand_state(rng, B, N, T, bc_scale=1.0):
-    u = rng.standard_normal((B, N, N)).astype(npdt(T))
-    f = rng.standard_normal((B, N, N)).astype(npdt(T))
+    hw = (N, N) if np.isscalar(N) else tuple(N)
+    u = rng.standard_normal((B,) + hw).astype(npdt(T))
+    f = rng.standard_normal((B,) + hw).astype(npdt(T))
     return u, f
 
 
@@ -107,10 +111,10 @@ def test_mg_sweep(T, problem, n, B):
     out = fr.get("b")
     close(out[:, 1:-1, 1:-1], (omd[fr.pid_np.astype(np.int64)] * f)[:, 1:-1, 1:-1], T, "zero sweep")
     # residual norm
-    ws = torch.zeros(_lib.norm_workspace_bytes(B, fr.N) // 8 + 1, dtype=torch.float64, device="cuda")
+    ws = torch.zeros(_lib.norm_workspace_bytes(B, fr.H, fr.W) // 8 + 1, dtype=torch.float64, device="cuda")
     res = torch.zeros(B, dtype=torch.float64, device="cuda")
     _lib.call("mg_residual_norm", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), fr.pid(), kt.data_ptr(), nt, res.data_ptr(),
-              ws.data_ptr(), *fr.args(), None)
+              ws.data_ptr(), *fr.args(), 0, 0, None)
     np.testing.assert_allclose(res.cpu().numpy(), orc.interior_norm(f - orc.knet_apply(u, fr.pid_np, ktab)),
                                rtol=1e-5 if T == torch.float32 else 1e-12)
 
@@ -402,8 +406,103 @@ def test_coarse_tail_kernel(T, problem, Nt, nlev, B, nu):
     if problem == "interface":
         maps = [ms.interface_pattern_map(((Nt - 1) >> k) + 1).reshape(-1) for k in range(nlev)]
         pidl = torch.from_numpy(np.concatenate(maps)).cuda()
-    _lib.call("mg_coarse_tail", T, fr.L.f.data_ptr(), fr.L.a.data_ptr(), Nt, nlev, fr.L.ld, fr.L.bs,
+    _lib.call("mg_coarse_tail", T, fr.L.f.data_ptr(), fr.L.a.data_ptr(), Nt, Nt, nlev, fr.L.ld, fr.L.bs,
               None if pidl is None else pidl.data_ptr(), kt.data_ptr(), om.data_ptr(), ktab.shape[0], rt.data_ptr(),
               pt.data_ptr(), 1.0, 1.0, nu[0], nu[1], 0, B, None)
     got = fr.get("a")
     close(got, ref, T, f"tail Nt={Nt} nlev={nlev} B={B} nu={nu}")
+
+
+# ----------------------------------------------------------------------------- rectangles (H != W)
+RECT = [(8, 16, 1), (64, 16, 2), (16, 256, 1), (512, 128, 1), (6, 10, 3)]
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("m,n,B", RECT)
+def test_mg_rect_kernels(T, m, n, B):
+    """Every framed kernel on an (m+1) x (n+1) grid (rows != columns: the local slabs of the
+    domain-decomposed path) against the oracle; the residual norm over a row range."""
+    from feanet_amd import _lib
+    rng = np.random.default_rng(7 * m + n)
+    fr = Frame(n, B, T, "poisson", m=m)
+    co = Frame(n // 2, B, T, "poisson", m=m // 2)
+    ktab, omd, R, P, kt, om, rt, pt = tables("poisson", T)
+    H, W = fr.H, fr.W
+    u, f = rand_state(rng, B, (H, W), T)
+    geo, _ = orc.square_geometry((H, W), npdt(T))
+    fr.put("a", u)
+    fr.put("f", f)
+    fr.put("b", u * 0 + 7.0)
+    _lib.call("mg_sweep", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), None, kt.data_ptr(),
+              om.data_ptr(), 1, *fr.args(), None)
+    up = orc.jacobi_sweep(u, f, fr.pid_np, ktab, geo, u * (1 - geo))
+    out = fr.get("b")
+    close(out[:, 1:-1, 1:-1], up[:, 1:-1, 1:-1], T, "rect sweep")
+    assert (out[:, 0, :] == 7).all() and (out[:, -1, :] == 7).all() and (out[:, :, -1] == 7).all()
+    w0, w1 = 1.25, 0.75
+    fr.put("b", u * 0 + 7.0)
+    _lib.call("mg_sweep_restrict", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), co.L.f.data_ptr(),
+              None, kt.data_ptr(), om.data_ptr(), 1, rt.data_ptr(), 1, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    close(fr.get("b")[:, 1:-1, 1:-1], up[:, 1:-1, 1:-1], T, "rect fused sweep")
+    close(co.get("f"), orc.restrict(f - orc.knet_apply(up, fr.pid_np, ktab), fr.pid_np, R, w0), T, "rect SR")
+    _lib.call("mg_residual_restrict", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), None, co.L.f.data_ptr(), None,
+              kt.data_ptr(), om.data_ptr(), 1, rt.data_ptr(), 1, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    close(co.get("f"), orc.restrict(f - orc.knet_apply(u, fr.pid_np, ktab), fr.pid_np, R, w0), T, "rect RR")
+    fr.put("b", u * 0)
+    _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), fr.L.b.data_ptr(), co.L.f.data_ptr(), None,
+              kt.data_ptr(), om.data_ptr(), 1, rt.data_ptr(), 1, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    v = omd[0] * f * geo
+    close(fr.get("b"), v, T, "rect zero-guess v")
+    close(co.get("f"), orc.restrict(f - orc.knet_apply(v, fr.pid_np, ktab), fr.pid_np, R, w0), T, "rect zero RR")
+    e = rng.standard_normal((B, co.H, co.W)).astype(npdt(T))
+    e[:, 0, :] = e[:, -1, :] = e[:, :, 0] = e[:, :, -1] = 0
+    co.put("a", e)
+    fr.put("b", u * 0 + 7.0)
+    _lib.call("mg_prolong_sweep", T, fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(),
+              None, None, kt.data_ptr(), om.data_ptr(), 1, pt.data_ptr(), 1, w1, *fr.args(), co.L.ld, co.L.bs, None)
+    x = u + orc.prolong(e, co.pid_np, P, w1)
+    ref = orc.jacobi_sweep(x, f, fr.pid_np, ktab, geo, u * (1 - geo))
+    close(fr.get("b")[:, 1:-1, 1:-1], ref[:, 1:-1, 1:-1], T, "rect prolong+sweep")
+    # residual norm over all interior rows and over a row range
+    ws = torch.zeros(_lib.norm_workspace_bytes(B, H, W) // 8 + 1, dtype=torch.float64, device="cuda")
+    res = torch.zeros(B, dtype=torch.float64, device="cuda")
+    r = f - orc.knet_apply(u, fr.pid_np, ktab)
+    for lo, hi in ((0, 0), (1, H - 1), (2, max(2, H // 2)), (H // 2, H - 1), (3, 3)):
+        _lib.call("mg_residual_norm", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), None, kt.data_ptr(), 1, res.data_ptr(),
+                  ws.data_ptr(), *fr.args(), lo, hi, None)
+        a, b = (1, H - 1) if (lo, hi) == (0, 0) else (lo, hi)
+        ref = np.sqrt((r[:, a:b, 1:-1].astype(np.float64) ** 2).sum(axis=(1, 2)))
+        np.testing.assert_allclose(res.cpu().numpy(), ref, rtol=1e-5 if T == torch.float32 else 1e-12,
+                                   err_msg=f"norm rows {lo}:{hi}")
+
+
+@pytest.mark.parametrize("T", [torch.float64, torch.float32])
+@pytest.mark.parametrize("m,n,tail", [(256, 128, True), (128, 256, True), (64, 128, False), (1024, 512, True)])
+def test_vcycle_rect_vs_oracle(T, m, n, tail):
+    """MultigridSolver(rows=m) on a rectangle against the oracle's V-cycle on the same grid."""
+    from feanet_amd.solver import MultigridSolver
+    rng = np.random.default_rng(m + n)
+    B = 2
+    H, W = m + 1, n + 1
+    s = MultigridSolver(n, rows=m, dtype=T, batch=B, coarse_tail=tail)
+    mg_o = orc.OracleMultigrid(n, "poisson", npdt(T), levels=s.L, rows=m)
+    assert s.L == mg_o.L
+    if tail:
+        assert s.tail_from is not None
+    u0 = rng.standard_normal((B, H, W)).astype(npdt(T))
+    f = rng.standard_normal((B, H, W)).astype(npdt(T))
+    geo, _ = orc.square_geometry((H, W), npdt(T))
+    s.set_rhs(f=torch.from_numpy(f).cuda().reshape(B, 1, H, W))
+    s.load(torch.from_numpy(u0).cuda().reshape(B, 1, H, W))
+    v = u0 * geo
+    r0 = orc.interior_norm(f - mg_o.levels[0].K(v))
+    for k in range(3):
+        s.vcycle()
+        v = mg_o.step(v, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        if T == torch.float64 or k == 0:
+            err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
+            assert err < (1e-10 if T == torch.float64 else 2e-5), f"cycle {k}: {err:.3e}"
+        np.testing.assert_allclose(s.residual_norm().cpu().numpy(), orc.interior_norm(f - mg_o.levels[0].K(v)),
+                                   rtol=1e-9 if T == torch.float64 else 2e-3,
+                                   atol=(1e-12 if T == torch.float64 else 1e-6) * r0.max())

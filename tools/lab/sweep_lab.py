@@ -19,7 +19,7 @@ s.load(torch.randn(1, 1, N, N, device="cuda", dtype=torch.float64, generator=g))
 L0 = s.levels[0]
 st = torch.cuda.current_stream()
 _lib.call("mg_sweep", s.dtype, L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, s.ktab.data_ptr(),
-          s.omd.data_ptr(), s.ntab, L0.B, L0.N, L0.ld, L0.bs, st.cuda_stream)
+          s.omd.data_ptr(), s.ntab, *L0.geom(), st.cuda_stream)
 ref = L0.b.clone()
 out = L0.a.clone()
 
@@ -35,7 +35,7 @@ def ev_time(fn, reps=40):
 
 bytes_ = 24 * (N - 2) ** 2
 prod = lambda: _lib.call("mg_sweep", s.dtype, L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None,
-                         s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab, L0.B, L0.N, L0.ld, L0.bs, st.cuda_stream)
+                         s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab, *L0.geom(), st.cuda_stream)
 res = []
 for rep in range(2):
     tp = ev_time(prod)
