@@ -1,0 +1,437 @@
+"""Domain-decomposed V-cycle over several MI355X GPUs: row slabs + halo exchange.
+
+The fine grid ((m+1) x (n+1) nodes, Poisson) is cut into P row slabs, one per rank (one process
+per GPU, torch.distributed over RCCL/xGMI).  Levels 0 .. Ld-1 are distributed; the level-Ld
+restriction is all-gathered and the rest of the V-cycle (levels >= Ld of the global grid) is solved
+redundantly on every rank by a single-GPU MultigridSolver, whose correction each rank copies back
+for its slab.  The result is bitwise the single-GPU V-cycle on the global grid (same kernels, same
+per-node arithmetic, same coarse schedule), which the tests check.
+
+Layout (class Partition).  Interior row offsets t_r = r * m / P split level 0; level l uses
+t_r / 2^l, so fine rows (2I-1, 2I) and coarse row I always live on the same rank.  Rank r owns
+global rows [s, e) = [1 + t_r, 1 + t_{r+1}) (the last rank up to H-1) and stores rows
+[gr0, gr0 + Hloc) with gr0 = t_r - G_l (0 on rank 0): G_l = G * 2^(Ld-l) ghost rows per side, the
+doubling keeping gr0_l = 2 gr0_{l+1} so the unmodified level kernels pair fine and coarse rows
+exactly as on one grid.  The level kernels compute every local interior row; ghost rows near the
+slab edge are refreshed by exchanges, deeper ones are redundant work (G_0 rows per side, a few %).
+
+Exchanges per V-cycle (depth = rows refreshed, 3 covers every kernel's reach):
+  after a sweep / prolongation-sweep on level l:   the new iterate of level l
+  after a residual-restriction on level l < Ld-1:  f_{l+1}
+  at level Ld:  all-gather of the owned rows of f_Ld -> the replicated coarse solve -> local copy
+i.e. 2*Ld - 1 neighbour exchanges (two 3-row messages per neighbour) and one all-gather.
+"""
+import torch
+
+from . import _lib
+from .schedule import vcycle_schedule
+from .solver import MultigridSolver
+
+DEPTH = 3  # rows per halo exchange
+
+
+def global_levels(m, n):
+    """Levels of the global grid (MultigridSolver's default for a rectangle)."""
+    L = 1
+    while n % (1 << L) == 0 and m % (1 << L) == 0 and (n >> L) >= 2 and (m >> L) >= 2:
+        L += 1
+    return L
+
+
+def default_agglomeration(m, n, P, L, max_nodes=1 << 20):
+    """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows."""
+    Ld = 1
+    while Ld < L - 1 and ((m >> Ld) + 1) * ((n >> Ld) + 1) > max_nodes and m % (P << (Ld + 1)) == 0 \
+            and m // (P << (Ld + 1)) >= 2:
+        Ld += 1
+    return Ld
+
+
+class LevelPart:
+    """Rank r's rows of one level: owned global rows [s, e), stored rows [gr0, gr0 + Hloc),
+    owned local rows [lo, hi)."""
+
+    def __init__(self, H, s, e, gr0, gend):
+        self.H, self.s, self.e, self.gr0 = H, s, e, gr0
+        self.Hloc = gend - gr0
+        self.lo, self.hi = s - gr0, e - gr0
+
+    def __repr__(self):
+        return f"LevelPart(H={self.H}, own=[{self.s},{self.e}), rows=[{self.gr0},{self.gr0 + self.Hloc}))"
+
+
+class Partition:
+    def __init__(self, m, n, P, Ld, G=2):
+        if P < 1 or Ld < 1:
+            raise ValueError("Partition: need P >= 1 and Ld >= 1")
+        if m % (P << Ld) or m // (P << Ld) < 2:
+            raise ValueError(f"Partition: {m} rows do not split into {P} slabs over {Ld} levels "
+                             f"(need m divisible by P*2^Ld with >= 2 coarse rows per rank)")
+        if n % (1 << Ld) or (n >> Ld) < 2:
+            raise ValueError(f"Partition: {n} columns do not coarsen {Ld} times")
+        self.m, self.n, self.P, self.Ld, self.G = m, n, P, Ld, G
+
+    def ghost(self, l):
+        return self.G << (self.Ld - l)
+
+    def rows_per_rank(self, l):
+        return (self.m // self.P) >> l
+
+    def level(self, l, r):
+        H = (self.m >> l) + 1
+        c = self.rows_per_rank(l)
+        g = self.ghost(l)
+        t = r * c
+        s = 1 + t
+        e = 1 + t + c if r < self.P - 1 else H - 1
+        gr0 = 0 if r == 0 else t - g
+        gend = H if r == self.P - 1 else e + g
+        return LevelPart(H, s, e, gr0, gend)
+
+
+def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a"):
+    """The distributed part of one V-cycle (levels 0..Ld-1) with its communication steps:
+    kernel steps of feanet_amd.schedule plus ("exchange", l, buf), ("gather",), ("coarse",),
+    ("scatter", dst)."""
+    steps, end = vcycle_schedule(Ld + 1, nu1, nu2, None, start, tail_from=Ld, fuse=fuse)
+    out = []
+    for st in steps:
+        kind, l = st[0], st[1]
+        if kind == "coarse_tail":
+            out += [("gather",), ("coarse",), ("scatter", st[2])]
+            continue
+        out.append(st)
+        if kind == "sweep":
+            out.append(("exchange", l, st[3]))
+        elif kind in ("prolong_sweep", "prolong_add"):
+            out.append(("exchange", l, st[4]))
+        elif kind in ("resid_restrict", "sweep_restrict") and l + 1 < Ld:
+            out.append(("exchange", l + 1, "f"))
+    return out, end
+
+
+def _rows(t, B, bs, ld, y0, y1):
+    """[B, (y1-y0)*ld] view of local rows y0..y1-1 of a framed buffer."""
+    return t.as_strided((B, (y1 - y0) * ld), (bs, 1), t.storage_offset() + (y0 + 1) * ld)
+
+
+class DDSolver:
+    """One rank of the domain-decomposed V-cycle.
+
+    Args: n, rows: global intervals (columns, rows) of the fine grid; rank, world: this rank and the
+    number of slabs; comm: a TorchComm (one process per GPU) or None when driven by a LocalGroup;
+    agglomerate: Ld (default: see default_agglomeration); other args as MultigridSolver (Poisson).
+    """
+
+    def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
+                 batch=1, nu1=1, nu2=1, fuse=True, graph=True):
+        self.n, self.m = n, rows
+        self.rank, self.P = rank, world
+        self.comm = comm
+        self.L = global_levels(rows, n)
+        self.Ld = default_agglomeration(rows, n, world, self.L) if agglomerate is None else int(agglomerate)
+        if not 1 <= self.Ld <= self.L - 1:
+            raise ValueError(f"DDSolver: agglomeration level {self.Ld} outside [1, {self.L - 1}]")
+        self.part = Partition(rows, n, world, self.Ld)
+        self.parts = [self.part.level(l, rank) for l in range(self.Ld + 1)]
+        self.dtype, self.B = dtype, batch
+        self.device = torch.device(device if device is not None else "cuda")
+        self.nu1, self.nu2, self.fuse = nu1, nu2, fuse
+        p0 = self.parts[0]
+        self.local = MultigridSolver(n, rows=p0.Hloc - 1, levels=self.Ld + 1, dtype=dtype, device=self.device,
+                                     batch=batch, nu1=nu1, nu2=nu2, fuse=fuse, coarse_tail=False, graph=False)
+        self.coarse = MultigridSolver(n >> self.Ld, rows=rows >> self.Ld, levels=self.L - self.Ld, dtype=dtype,
+                                      device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse,
+                                      coarse_tail=True, graph=False, zero_start=True)
+        for l, lp in enumerate(self.parts):
+            Lv = self.local.levels[l]
+            assert Lv.H == lp.Hloc and Lv.W == (n >> l) + 1, (l, Lv.H, lp)
+        self.coarse_plan, self.coarse_end = self.coarse._build("a")
+        self.use_graph = graph
+        self._segs = {}
+        self._graphs = {}
+        self._state = "a"
+        self.norm_sq = torch.zeros(batch, dtype=torch.float64, device=self.device)
+
+    # ------------------------------------------------------------------ data
+    @property
+    def H(self):
+        return self.m + 1
+
+    @property
+    def W(self):
+        return self.n + 1
+
+    def _local_rows(self, x):
+        """Rows [gr0, gr0 + Hloc) of a global [B, 1, H, W] tensor, contiguous."""
+        p0 = self.parts[0]
+        x = x.to(self.device, self.dtype).reshape(-1, 1, self.H, self.W)
+        if x.shape[0] == 1 and self.B > 1:
+            x = x.expand(self.B, 1, self.H, self.W)
+        return x[:, :, p0.gr0:p0.gr0 + p0.Hloc].contiguous()
+
+    def set_rhs(self, f):
+        """Assembled right-hand side of the GLOBAL problem, [B, 1, H, W] (any device)."""
+        self.local._pack(self._local_rows(f), self.local.levels[0].f, reset=False)
+
+    def load(self, u0=None, bc=None):
+        """Global initial iterate (zero by default), reset_boundary applied: u0 * geo + bc
+        (jacobi.py:27-29; square geometry, bc = Dirichlet data, zero inside)."""
+        H, W = self.H, self.W
+        u = torch.zeros((self.B, 1, H, W), dtype=self.dtype, device=self.device) if u0 is None else \
+            u0.to(self.device, self.dtype).reshape(-1, 1, H, W).expand(self.B, 1, H, W)
+        u = u * (1 - _boundary_mask(H, W, u))
+        if bc is not None:
+            u = u + bc.to(self.device, self.dtype).reshape(-1, 1, H, W)
+        x = self._local_rows(u)
+        L0 = self.local.levels[0]
+        self.local._pack(x, L0.a, reset=False)
+        self.local._pack(x, L0.b, reset=False)
+        self._state = "a"
+
+    def owned_solution(self):
+        """(s, e, u[B, 1, e-s, W]): the current iterate on the rows this rank owns."""
+        p0 = self.parts[0]
+        L0 = self.local.levels[0]
+        v = L0.view(L0.buf(self._state))
+        return p0.s, p0.e, v[:, p0.lo:p0.hi].unsqueeze(1).clone()
+
+    def residual_norm_sq_local(self):
+        """Sum over owned rows of (f - K u)^2 per sample (float64 device tensor [B])."""
+        L0 = self.local.levels[0]
+        p0 = self.parts[0]
+        loc = self.local
+        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(), None,
+                  loc.ktab.data_ptr(), loc.ntab, loc.norm_out.data_ptr(), loc.ws.data_ptr(), *L0.geom(),
+                  p0.lo, p0.hi, torch.cuda.current_stream(self.device).cuda_stream)
+        return loc.norm_out * loc.norm_out
+
+    # ------------------------------------------------------------------ plan
+    def segments(self, start):
+        """One V-cycle as [("k", [(name, args), ...]) | ("c", comm step)], and the end buffer."""
+        if start not in self._segs:
+            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, start)
+            segs = []
+            for st in steps:
+                if st[0] in ("exchange", "gather", "scatter"):
+                    segs.append(("c", st))
+                    continue
+                launches = list(self.coarse_plan) if st[0] == "coarse" else [self.local.bind_step(st)]
+                if segs and segs[-1][0] == "k":
+                    segs[-1][1].extend(launches)
+                else:
+                    segs.append(("k", launches))
+            self._segs[start] = (segs, end)
+        return self._segs[start]
+
+    def run_kernels(self, start, i):
+        """Kernel segment i of the cycle starting in `start` (graph-replayed after its first run)."""
+        segs, _ = self.segments(start)
+        launches = segs[i][1]
+        key = (start, i)
+        stream = torch.cuda.current_stream(self.device)
+        if not self.use_graph or key not in self._graphs:
+            if self.use_graph:
+                self._graphs[key] = None  # eager once, capture on the second use
+            for name, args in launches:
+                _lib.call(name, self.dtype, *args, stream.cuda_stream)
+            return
+        g = self._graphs[key]
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(stream)
+            with torch.cuda.graph(g, stream=s):
+                for name, args in launches:
+                    _lib.call(name, self.dtype, *args, s.cuda_stream)
+            stream.wait_stream(s)
+            self._graphs[key] = g
+        g.replay()
+
+    # buffers the communication steps touch
+    def level_rows(self, l, name, y0, y1):
+        Lv = self.local.levels[l]
+        return _rows(Lv.buf(name), Lv.B, Lv.bs, Lv.ld, y0, y1)
+
+    def gather_source(self):
+        """Owned rows of f_Ld, padded to rows_per_rank (the last rank adds the zero boundary row)."""
+        pl = self.parts[self.Ld]
+        c = self.part.rows_per_rank(self.Ld)
+        return self.level_rows(self.Ld, "f", pl.lo, pl.lo + c)
+
+    def gather_target(self):
+        """Rows [1, 1 + P*c) of the coarse solver's top-level f: the P gathered chunks in rank order."""
+        Lc = self.coarse.levels[0]
+        c = self.part.rows_per_rank(self.Ld)
+        return _rows(Lc.f, Lc.B, Lc.bs, Lc.ld, 1, 1 + self.P * c)
+
+    def scatter(self, dst):
+        """Copy this rank's rows of the coarse solution into level Ld's buffer `dst`."""
+        pl = self.parts[self.Ld]
+        Lc = self.coarse.levels[0]
+        src = _rows(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc)
+        self.level_rows(self.Ld, dst, 0, pl.Hloc).copy_(src)
+
+    # ------------------------------------------------------------------ driver (one process per rank)
+    def vcycle(self, k=1):
+        if self.comm is None:
+            raise RuntimeError("DDSolver.vcycle: no communicator (use LocalGroup for in-process ranks)")
+        for _ in range(k):
+            segs, end = self.segments(self._state)
+            for i, (kind, st) in enumerate(segs):
+                if kind == "k":
+                    self.run_kernels(self._state, i)
+                elif st[0] == "exchange":
+                    self.comm.exchange(self, st[1], st[2])
+                elif st[0] == "gather":
+                    self.comm.allgather(self.gather_target(), self.gather_source())
+                elif st[0] == "scatter":
+                    self.scatter(st[1])
+            self._state = end
+
+    def residual_norm(self):
+        n2 = self.residual_norm_sq_local()
+        if self.comm is not None:
+            n2 = self.comm.allreduce_sum(n2)
+        return torch.sqrt(n2)
+
+
+def _boundary_mask(H, W, like):
+    m = torch.zeros((H, W), dtype=like.dtype, device=like.device)
+    m[0, :] = 1
+    m[-1, :] = 1
+    m[:, 0] = 1
+    m[:, -1] = 1
+    return m
+
+
+class TorchComm:
+    """Halo exchange / all-gather / all-reduce over torch.distributed.  With the nccl backend (RCCL
+    on ROCm) device buffers are sent directly; with gloo they are staged through host memory."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.gpu = dist.get_backend(group) == "nccl"
+
+    def _stage(self, t):
+        return t.contiguous() if self.gpu else t.cpu()
+
+    def exchange(self, s, l, name):
+        dist = self.dist
+        lp = s.parts[l]
+        d = DEPTH
+        sends, recvs = [], []
+        if s.rank > 0:
+            sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
+            recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
+        if s.rank < s.P - 1:
+            sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
+            recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
+        sbufs = [(self._stage(t), peer) for t, peer in sends]
+        rbufs = [(t if (self.gpu and t.is_contiguous()) else
+                  torch.empty(t.shape, dtype=t.dtype, device=t.device if self.gpu else "cpu"), t, peer)
+                 for t, peer in recvs]
+        ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, peer in sbufs]
+        ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, _, peer in rbufs]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for b, t, _ in rbufs:
+            if b is not t:
+                t.copy_(b)
+
+    def allgather(self, target, source):
+        dist = self.dist
+        if self.gpu and target.is_contiguous() and source.is_contiguous():
+            dist.all_gather_into_tensor(target.reshape(-1), source.reshape(-1), group=self.group)
+            return
+        src = self._stage(source)
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src, group=self.group)
+        B = source.shape[0]
+        full = torch.stack([p.reshape(B, -1) for p in parts], 1).reshape(B, -1)
+        target.copy_(full)
+
+    def allreduce_sum(self, t):
+        if self.gpu:
+            self.dist.all_reduce(t, group=self.group)
+            return t
+        c = t.cpu()
+        self.dist.all_reduce(c, group=self.group)
+        return c.to(t.device)
+
+
+class LocalGroup:
+    """All P ranks in one process (one device): the same schedule executed in lockstep with the
+    exchanges done as device copies.  Used to test the decomposition on a single GPU."""
+
+    def __init__(self, n, rows, world, **kw):
+        self.ranks = [DDSolver(n, rows, r, world, comm=None, **kw) for r in range(world)]
+
+    def set_rhs(self, f):
+        for s in self.ranks:
+            s.set_rhs(f)
+
+    def load(self, u0=None, bc=None):
+        for s in self.ranks:
+            s.load(u0, bc)
+
+    def vcycle(self, k=1):
+        for _ in range(k):
+            start = self.ranks[0]._state
+            segs, end = self.ranks[0].segments(start)
+            for i, (kind, st) in enumerate(segs):
+                if kind == "k":
+                    for s in self.ranks:
+                        s.segments(start)
+                        s.run_kernels(start, i)
+                elif st[0] == "exchange":
+                    self._exchange(st[1], st[2])
+                elif st[0] == "gather":
+                    chunks = [s.gather_source() for s in self.ranks]
+                    for s in self.ranks:
+                        tgt = s.gather_target()
+                        c = chunks[0].shape[1]
+                        for r, ch in enumerate(chunks):
+                            tgt[:, r * c:(r + 1) * c].copy_(ch)
+                elif st[0] == "scatter":
+                    for s in self.ranks:
+                        s.scatter(st[1])
+            for s in self.ranks:
+                s._state = end
+
+    def _exchange(self, l, name):
+        d = DEPTH
+        for r, s in enumerate(self.ranks):
+            lp = s.parts[l]
+            if r > 0:
+                q = self.ranks[r - 1]
+                qp = q.parts[l]
+                s.level_rows(l, name, lp.lo - d, lp.lo).copy_(q.level_rows(l, name, qp.hi - d, qp.hi))
+            if r < len(self.ranks) - 1:
+                q = self.ranks[r + 1]
+                qp = q.parts[l]
+                s.level_rows(l, name, lp.hi, lp.hi + d).copy_(q.level_rows(l, name, qp.lo, qp.lo + d))
+
+    def solution(self):
+        """Global iterate assembled from the owned rows (boundary rows from ranks 0 / P-1)."""
+        s0 = self.ranks[0]
+        out = torch.zeros((s0.B, 1, s0.H, s0.W), dtype=s0.dtype, device=s0.device)
+        for s in self.ranks:
+            a, b, u = s.owned_solution()
+            out[:, :, a:b] = u
+            L0 = s.local.levels[0]
+            v = L0.view(L0.buf(s._state))
+            p0 = s.parts[0]
+            if s.rank == 0:
+                out[:, 0, 0] = v[:, 0]
+            if s.rank == s.P - 1:
+                out[:, 0, -1] = v[:, p0.Hloc - 1]
+        return out
+
+    def residual_norm(self):
+        return torch.sqrt(sum(s.residual_norm_sq_local() for s in self.ranks))

@@ -28,10 +28,12 @@ def _other(b):
     return "b" if b == "a" else "a"
 
 
-def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fuse=True):
+def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fuse=True, top_zero=False):
     """tail_from = t (1 <= t <= L-1): levels t..L-1 run as one coarse_tail step.
     fuse: the last pre-sweep of a level with a given iterate runs fused with its residual and
-    restriction (sweep_restrict)."""
+    restriction (sweep_restrict).
+    top_zero: level 0 starts from a zero guess like the coarse levels (the coarse sub-cycle of a
+    domain-decomposed V-cycle, run on the agglomerated level; bitwise the single-grid coarse part)."""
     if tail_from is not None and not (1 <= tail_from <= L - 1):
         raise ValueError("vcycle_schedule: tail_from must be in [1, L-1]")
     if L < 1 or nu1 < 0 or nu2 < 0:
@@ -40,7 +42,7 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
         raise ValueError(f"vcycle_schedule: unknown compat mode {compat!r}")
     steps = []
     cur = ["zero"] * L
-    cur[0] = start
+    cur[0] = "zero" if top_zero else start
 
     def sweep(l, zero=False):
         dst = "a" if (zero or cur[l] == "zero") else _other(cur[l])
@@ -74,7 +76,12 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
             steps.append(("resid_restrict", l, cur[l], None))
 
     # ---- down
-    presmooth_restrict(0, nu1, False)
+    if top_zero and nu1 > 0 and not q2:
+        presmooth_restrict(0, nu1, True)
+    elif top_zero:
+        steps.append(("resid_restrict", 0, "zero", None))
+    else:
+        presmooth_restrict(0, nu1, False)
     if q2:
         for _ in range((L - 1) * nu1):
             sweep(0)

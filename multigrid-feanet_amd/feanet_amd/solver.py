@@ -90,11 +90,13 @@ class MultigridSolver:
             (fea_mg_coarse_tail); False keeps one launch per level op.
         fuse: run the last pre-sweep of a level fused with its residual + restriction
             (fea_mg_sweep_restrict, one read of u and f); False issues them separately.
+        zero_start: every V-cycle starts the finest level from a zero guess too (the replicated coarse
+            sub-solve of the domain-decomposed path, feanet_amd.dd).
     """
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
-                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None):
+                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -124,6 +126,7 @@ class MultigridSolver:
         self.compat = compat
         self.use_graph = graph
         self.fuse = fuse
+        self.zero_start = zero_start
         npdt = np.float32 if dtype == torch.float32 else np.float64
         multi = problem == "interface"
         if problem not in ("poisson", "interface"):
@@ -279,8 +282,13 @@ class MultigridSolver:
     def _build(self, start):
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
+        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
+                                     top_zero=self.zero_start)
+        return [self.bind_step(st) for st in steps], end
+
+    def bind_step(self, st):
+        """One schedule step -> (C-ABI function base name, args without the stream)."""
         lv = self.levels
-        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse)
         kt, om, nt = self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab
         rt, pt = self.rtab.data_ptr(), self.ptab.data_ptr()
         nr, npt = self.rtab.shape[0], self.ptab.shape[0]
@@ -297,33 +305,29 @@ class MultigridSolver:
         def cgeom(l):
             return (lv[l + 1].ld, lv[l + 1].bs)
 
-        plan = []
-        for st in steps:
-            kind, l = st[0], st[1]
-            f = lv[l].f.data_ptr()
-            if kind == "sweep":
-                plan.append(("mg_sweep", (ptr(l, st[2]), f, ptr(l, st[3]), pid(l), kt, om, nt) + geom(l)))
-            elif kind == "resid_restrict":
-                plan.append(("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
-                                                      kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l)))
-            elif kind == "sweep_restrict":
-                plan.append(("mg_sweep_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
-                                                   kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l)))
-            elif kind == "prolong_sweep":
-                plan.append(("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
-                                                  pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l)))
-            elif kind == "prolong_add":
-                plan.append(("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
-                                                self.w[1]) + geom(l) + cgeom(l)))
-            elif kind == "coarse_tail":
-                t = l
-                plan.append(("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
-                                                lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
-                                                kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
-                                                int(self.compat == "mm_interface_q2"), lv[t].B)))
-            else:  # pragma: no cover
-                raise AssertionError(kind)
-        return plan, end
+        kind, l = st[0], st[1]
+        f = lv[l].f.data_ptr()
+        if kind == "sweep":
+            return ("mg_sweep", (ptr(l, st[2]), f, ptr(l, st[3]), pid(l), kt, om, nt) + geom(l))
+        if kind == "resid_restrict":
+            return ("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
+                                             kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
+        if kind == "sweep_restrict":
+            return ("mg_sweep_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
+                                          kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
+        if kind == "prolong_sweep":
+            return ("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
+                                         pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l))
+        if kind == "prolong_add":
+            return ("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
+                                       self.w[1]) + geom(l) + cgeom(l))
+        if kind == "coarse_tail":
+            t = l
+            return ("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
+                                       lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
+                                       kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
+                                       int(self.compat == "mm_interface_q2"), lv[t].B))
+        raise ValueError(f"MultigridSolver: unknown schedule step {kind!r}")
 
     def _plan(self, start):
         if start not in self._plans:

@@ -1,0 +1,90 @@
+"""Domain decomposition (feanet_amd.dd) on the CPU: partition invariants, the
+communication schedule, and a world_size 2 / 3 gloo run of the decomposed V-cycle (oracle
+operators on each rank's slab) against the oracle's single-grid V-cycle on the global grid."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from feanet_amd.dd import DEPTH, Partition, dd_schedule, default_agglomeration, global_levels
+from oracle import feanet_oracle as orc
+
+
+@pytest.mark.parametrize("m,n,P,Ld", [(64, 32, 2, 2), (96, 64, 3, 3), (256, 128, 4, 3), (4096, 4096, 8, 4),
+                                      (16384, 8192, 8, 4), (512, 512, 1, 3), (48, 16, 3, 2)])
+def test_partition_invariants(m, n, P, Ld):
+    part = Partition(m, n, P, Ld)
+    for l in range(Ld + 1):
+        H = (m >> l) + 1
+        owned = []
+        for r in range(P):
+            p = part.level(l, r)
+            owned += list(range(p.s, p.e))
+            assert 0 <= p.gr0 and p.gr0 + p.Hloc <= H and p.Hloc % 2 == 1 and p.Hloc >= 3
+            assert 1 <= p.lo and p.hi <= p.Hloc - 1
+            if l < Ld:
+                q = part.level(l + 1, r)
+                assert p.gr0 == 2 * q.gr0 and p.Hloc == 2 * q.Hloc - 1  # fine (2I-1, 2I) <-> coarse I locally
+                assert p.s == 2 * q.s - 1  # coarse row I owned with its fine rows (2I-1, 2I)
+                assert p.e == (2 * q.e - 1 if r < P - 1 else H - 1)
+                if r > 0:
+                    assert p.lo >= DEPTH + 1  # exchanged rows + one kept edge row
+                if r < P - 1:
+                    assert p.Hloc - p.hi >= DEPTH + 1
+                assert p.e - p.s >= DEPTH
+        assert owned == list(range(1, H - 1)), "interior rows owned exactly once"
+
+
+def test_partition_rejects_bad_splits():
+    with pytest.raises(ValueError):
+        Partition(100, 64, 3, 2)
+    with pytest.raises(ValueError):
+        Partition(64, 64, 8, 3)  # 1 coarse row per rank
+
+
+def test_dd_schedule_comm_counts():
+    for Ld in (1, 2, 3, 5):
+        steps, end = dd_schedule(Ld)
+        kinds = [s[0] for s in steps]
+        assert kinds.count("exchange") == 2 * Ld - 1
+        assert kinds.count("gather") == kinds.count("coarse") == kinds.count("scatter") == 1
+        assert end in ("a", "b")
+
+
+def test_default_agglomeration():
+    L = global_levels(16384, 8192)
+    Ld = default_agglomeration(16384, 8192, 8, L)
+    assert ((16384 >> Ld) + 1) * ((8192 >> Ld) + 1) <= (1 << 20)
+    Partition(16384, 8192, 8, Ld)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, m, n, Ld, port, outdir):
+    import dd_oracle
+    dd_oracle.run_rank(rank, world, m, n, Ld, port, outdir)
+
+
+@pytest.mark.parametrize("m,n,P,Ld", [(64, 32, 2, 2), (96, 32, 3, 2), (128, 64, 2, 3)])
+def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld):
+    import dd_oracle
+    mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path)), nprocs=P, join=True)
+    got = np.concatenate([np.load(os.path.join(tmp_path, f"rank{r}.npy")) for r in range(P)], axis=1)
+    f, u = dd_oracle.problem(m, n, 2)
+    L = global_levels(m, n)
+    mg = orc.OracleMultigrid(n, "poisson", np.float64, levels=L, rows=m)
+    geo, _ = orc.square_geometry((m + 1, n + 1), np.float64)
+    mg.set_boundary(geo, u * (1 - geo))
+    v = u
+    for _ in range(2):
+        v = mg.step(v, f)
+    err = np.abs(got - v[:, 1:-1]).max() / np.abs(v).max()
+    assert err < 1e-13, err

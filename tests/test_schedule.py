@@ -21,17 +21,17 @@ def interpret(mg, steps, v, f, compat=None):
 
     def get(l, name):
         if name == "zero":
-            return np.zeros((B, lv[l].N, lv[l].N), dt)
+            return np.zeros((B, lv[l].H, lv[l].W), dt)
         return bufs[l][name]
 
     for st in steps:
         kind, l = st[0], st[1]
         if kind == "sweep":
-            src = np.zeros((B, lv[l].N, lv[l].N), dt) if st[2] is None else get(l, st[2])
+            src = np.zeros((B, lv[l].H, lv[l].W), dt) if st[2] is None else get(l, st[2])
             bufs[l][st[3]] = lv[l].sweep(src, fs[l])
         elif kind == "resid_restrict":
             if st[2] is None:
-                src = lv[l].sweep(np.zeros((B, lv[l].N, lv[l].N), dt), fs[l])
+                src = lv[l].sweep(np.zeros((B, lv[l].H, lv[l].W), dt), fs[l])
                 bufs[l][st[3]] = src
             else:
                 src = get(l, st[2])
@@ -66,7 +66,7 @@ def tail_oracle(mg, t, f_t, compat, B, nu1=None, nu2=None, q2=None):
     q2 = mg.q2 if q2 is None else q2
     lv = mg.levels[t:]
     dt = mg.dtype
-    zeros = lambda k: np.zeros((B, lv[k].N, lv[k].N), dt)
+    zeros = lambda k: np.zeros((B, lv[k].H, lv[k].W), dt)
     f = [f_t] + [None] * (len(lv) - 1)
     v = [zeros(k) for k in range(len(lv))]
     for k in range(len(lv) - 1):
