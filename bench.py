@@ -15,9 +15,11 @@ Also reported on the same JSON line:
   cpu_baseline  the CPU oracle (numpy restatement of the reference V-cycle, 1 thread) on the same
                 workload, a bounded sample of whole V-cycles, rank 0 at N = 1 only.
 
-Multi-GPU (torchrun, one process per GPU): each rank runs its own 4097^2 problem (weak scaling,
-replicas; the domain-decomposed 8193^2 path is bench --config dd8193).  Timing: barrier +
-synchronize on both sides of the K steps, max over ranks.
+Multi-GPU (torchrun, one process per GPU): domain decomposition (feanet_amd.dd) of one global grid
+that grows with the GPU count at a fixed 4096 x 4096 intervals per GPU (weak scaling: 4097^2,
+8193x4097, 8193^2, 16385x8193 for 1, 2, 4, 8 GPUs), row slabs with RCCL halo exchange and an
+agglomerated coarse solve; value = global DoF / t_step.  --mode replicas runs independent
+problems instead.  Timing: barrier + synchronize on both sides of the K steps, max over ranks.
 """
 import argparse
 import json
@@ -40,16 +42,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_init():
+def dist_init(force=False):
+    """One process per GPU (torchrun env).  force: create the process group even for one rank (the
+    domain-decomposed path always talks through torch.distributed)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
-        torch.cuda.set_device(local)
+    torch.cuda.set_device(local)
+    if ws > 1 or force:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(ws))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
     return ws, rank
 
 
@@ -143,28 +149,67 @@ def cpu_baseline(n, seconds_budget=20.0):
                       f"workload by the numpy oracle (oracle/feanet_oracle.py), 1 thread, host of the GPU box"}
 
 
+def dd_domain(P, n0):
+    """Weak-scaled global grid for P slabs of n0 x n0 intervals each, aspect ratio <= 2 when P is a
+    power of two: 1 -> n0 x n0, 2 -> 2n0 x n0, 4 -> 2n0 x 2n0, 8 -> 4n0 x 2n0 (rows x columns)."""
+    if P & (P - 1) == 0:
+        k = P.bit_length() - 1
+        return n0 << ((k + 1) // 2), n0 << (k // 2)
+    return n0 * P, n0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=4096, help="intervals per edge (N = n+1 nodes)")
+    ap.add_argument("--n", type=int, default=4096, help="intervals per edge (N = n+1 nodes); per GPU in dd mode")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--problem", default="poisson", choices=["poisson", "interface"])
+    ap.add_argument("--mode", default=None, choices=["single", "dd", "replicas"],
+                    help="default: single at 1 GPU, dd (domain decomposition, weak scaling) at N > 1")
+    ap.add_argument("--agglomerate", type=int, default=None, help="dd: level gathered for the coarse solve")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     args = ap.parse_args()
 
-    ws, rank = dist_init()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    mode = args.mode or ("dd" if ws > 1 else "single")
+    ws, rank = dist_init(force=(mode == "dd"))
     from feanet_amd.solver import MultigridSolver
     T = torch.float64 if args.dtype == "f64" else torch.float32
     n, B = args.n, args.batch
-    N = n + 1
-    s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
     g = torch.Generator(device="cuda")
-    g.manual_seed(1234 + rank)
-    s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
+    if mode == "dd":
+        if args.problem != "poisson":
+            raise SystemExit("bench: the domain-decomposed path runs the Poisson problem")
+        from feanet_amd.dd import DDSolver, TorchComm
+        m, nc = dd_domain(ws, n)
+        s = DDSolver(nc, m, rank, ws, comm=TorchComm(), agglomerate=args.agglomerate, dtype=T, batch=B)
+        g.manual_seed(1234)  # one global problem: every rank draws the same rhs and keeps its rows
+        f = torch.randn(B, 1, m + 1, nc + 1, device="cuda", dtype=T, generator=g)
+        s.set_rhs(f)
+        del f
+        torch.cuda.empty_cache()
+        dof = B * (m + 1) * (nc + 1)
+        lvl = s.local
+        p0 = s.parts[0]
+        workload = (f"{m + 1}x{nc + 1} poisson {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
+                    f"{ws} row slabs of {p0.e - p0.s} rows (+ghosts) x {nc + 1}, levels >= {s.Ld} agglomerated, "
+                    f"batch {B}")
+        parallelism = (f"dd{ws}: row slabs, RCCL halo exchange ({2 * s.Ld - 1} per V-cycle) + all-gather of "
+                       f"level {s.Ld}, redundant coarse solve")
+    else:
+        N = n + 1
+        s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
+        g.manual_seed(1234 + rank)
+        s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
+        dof = B * N * N * ws
+        lvl = s
+        workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics), "
+                    f"batch {B} per GPU")
+        parallelism = "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"
     s.load()
     # contraction factor over the first 8 cycles (before the fp64 floor), then restart from zero
     r0 = s.residual_norm()
@@ -185,16 +230,17 @@ def main():
     t = time.perf_counter() - t0
     t = max_over_ranks(t, ws)
     ms_step = t / args.steps * 1e3
-    dof = B * N * N * ws
     value = dof / (t / args.steps)
 
-    fine = time_fine_kernels(s, args.kernel_reps)
+    fine = time_fine_kernels(lvl, args.kernel_reps)
     kt, kbytes = fine["fea_mg_sweep"]
     kt = max_over_ranks(kt, ws)
     achieved = kbytes / kt / 1e9
-    traffic, tsrc = (load_traffic("mg_sweep_f64_4097") if (N == 4097 and B == 1 and args.dtype == "f64"
-                                                             and args.problem == "poisson") else (None, None))
-    vbytes = s.bytes_per_vcycle()
+    L0 = lvl.levels[0]
+    traffic, tsrc = (load_traffic("mg_sweep_f64_4097") if (mode == "single" and L0.H == 4097 and L0.W == 4097
+                                                            and B == 1 and args.dtype == "f64"
+                                                            and args.problem == "poisson") else (None, None))
+    vbytes = s.bytes_per_vcycle() if mode == "single" else None
 
     rec = {
         "metric": METRIC,
@@ -209,31 +255,29 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded Gaussian rhs, zero initial guess)",
-        "config": {"workload": f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) "
-                               f"(MultiGrid.Step semantics), batch {B} per GPU",
-                   "nodes_per_edge": N, "batch": B, "levels": s.L,
-                   "parallelism": "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "fea_mg_sweep (fine-level Ke-stencil Jacobi sweep, 4097^2 fp64)",
+        "config": {"workload": workload, "mode": mode, "batch": B, "levels": s.L, "parallelism": parallelism},
+        "roofline": {"bound": "hbm",
+                     "kernel": f"fea_mg_sweep (fine-level Ke-stencil Jacobi sweep, {L0.H}x{L0.W} {args.dtype})",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": kt * 1e6,
                      "algorithmic_bytes_per_launch": kbytes},
-        "fine_level_kernels": {k: {"avg_launch_us": t * 1e6, "algorithmic_bytes": nb,
-                                   "achieved_GBps": nb / t / 1e9, "frac": nb / t / 1e9 / HBM_PEAK_GBS}
-                               for k, (t, nb) in fine.items()},
-        "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if ws == 1 else None,
+        "fine_level_kernels": {k: {"avg_launch_us": tk * 1e6, "algorithmic_bytes": nb,
+                                   "achieved_GBps": nb / tk / 1e9, "frac": nb / tk / 1e9 / HBM_PEAK_GBS}
+                               for k, (tk, nb) in fine.items()},
+        "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if (ws == 1 and vbytes) else None,
         "vcycle_algorithmic_bytes": vbytes,
         "residual_contraction_per_cycle": conv,
     }
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.problem == "poisson" and B == 1:
+    if rank == 0 and ws == 1 and mode == "single" and not args.no_cpu_baseline and args.problem == "poisson" \
+            and B == 1:
         log("[bench] timing the CPU oracle baseline ...")
         rec["cpu_baseline"] = cpu_baseline(n)
     elif rank == 0:
         rec["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
