@@ -202,6 +202,20 @@ int fea_mg_residual_norm_f64(const double* u, const double* f, const uint8_t* pi
                              double* out, double* ws, int B, int H, int W, int ld, long long bstride, int rlo,
                              int rhi, void* stream);
 
+/* One sweep of the learned smoother (HJacIterator.HRelax, M-FEANet-mg_test.ipynb:147-155, HNet
+ * :97-106) fused in one pass:  j = J(u, f);  d = (W_nl * .. (W_1 * (j - u)) .g ..) .g;  out = j + d
+ * on the interior (boundary untouched).  hw = nlayers 3x3 conv weights (cross-correlation, zero
+ * padding; nlayers <= 3), g = interior mask.  u == NULL: zero initial guess (coarse levels).
+ * u_raw (optional, framed like u): the iterate as the caller passed it before reset_boundary — the
+ * reference forms j - u with the un-reset u, so a first sweep from a guess whose boundary is not the
+ * Dirichlet data sees (bc - u_raw) on the boundary nodes; NULL = u already holds the boundary. */
+int fea_mg_hsweep_f32(const float* u, const float* u_raw, const float* f, float* out, const uint8_t* pid,
+                      const float* ktab, const float* omd, int ntab, const float* hw, int nlayers, int B, int H,
+                      int W, int ld, long long bstride, void* stream);
+int fea_mg_hsweep_f64(const double* u, const double* u_raw, const double* f, double* out, const uint8_t* pid,
+                      const double* ktab, const double* omd, int ntab, const double* hw, int nlayers, int B,
+                      int H, int W, int ld, long long bstride, void* stream);
+
 /* The whole coarse end of the V-cycle (levels t..t+nlev-1 of an Ht x Wt level, Ht, Wt <= 65 and
  * (Ht-1), (Wt-1) divisible by 2^(nlev-1)) in ONE launch,
  * one 1024-thread workgroup per sample, every level resident in LDS.  Input f_t and output v_t

@@ -1402,7 +1402,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (rhi == rlo) {                                                                                        \
-      hipMemsetAsync(ws, 0, sizeof(double) * (size_t)B * g.nstrips, s);                                      \
+      (void)hipMemsetAsync(ws, 0, sizeof(double) * (size_t)B * g.nstrips, s);                                      \
       g.ntr = 1;                                                                                             \
     } else if (ntab > 1) {                                                                                   \
       k_mg_resnorm<T, true><<<grid, 256, 0, s>>>(g);                                                         \

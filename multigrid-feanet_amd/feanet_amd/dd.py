@@ -321,27 +321,45 @@ class TorchComm:
         return t.contiguous() if self.gpu else t.cpu()
 
     def exchange(self, s, l, name):
+        """Refresh DEPTH ghost rows on both sides of rank s's slab of level l buffer `name`.  The
+        P2P op lists are built once per (level, buffer) and reused (fixed device views)."""
         dist = self.dist
-        lp = s.parts[l]
-        d = DEPTH
-        sends, recvs = [], []
-        if s.rank > 0:
-            sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
-            recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
-        if s.rank < s.P - 1:
-            sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
-            recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
-        sbufs = [(self._stage(t), peer) for t, peer in sends]
-        rbufs = [(t if (self.gpu and t.is_contiguous()) else
-                  torch.empty(t.shape, dtype=t.dtype, device=t.device if self.gpu else "cpu"), t, peer)
-                 for t, peer in recvs]
-        ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, peer in sbufs]
-        ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, _, peer in rbufs]
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-        for b, t, _ in rbufs:
-            if b is not t:
+        key = (id(s), l, name)
+        plan = self._plans.get(key) if hasattr(self, "_plans") else None
+        if plan is None:
+            if not hasattr(self, "_plans"):
+                self._plans = {}
+            lp = s.parts[l]
+            d = DEPTH
+            sends, recvs = [], []
+            if s.rank > 0:
+                sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
+                recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
+            if s.rank < s.P - 1:
+                sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
+                recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
+            direct = self.gpu and all(t.is_contiguous() for t, _ in sends + recvs)
+            if direct:
+                sb = [t for t, _ in sends]
+                rb = [t for t, _ in recvs]
+            else:
+                dev = sends[0][0].device if (sends and self.gpu) else "cpu"
+                sb = [torch.empty(t.shape, dtype=t.dtype, device=dev) for t, _ in sends]
+                rb = [torch.empty(t.shape, dtype=t.dtype, device=dev) for t, _ in recvs]
+            ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, (_, peer) in zip(sb, sends)]
+            ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, (_, peer) in zip(rb, recvs)]
+            plan = (ops, direct, list(zip(sb, [t for t, _ in sends])), list(zip(rb, [t for t, _ in recvs])))
+            self._plans[key] = plan
+        ops, direct, spairs, rpairs = plan
+        if not ops:
+            return
+        if not direct:
+            for b, t in spairs:
+                b.copy_(t)
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        if not direct:
+            for b, t in rpairs:
                 t.copy_(b)
 
     def allgather(self, target, source):

@@ -114,3 +114,43 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
         for _ in range(max(nu2 - 1, 0)):
             sweep(l)
     return steps, cur[0]
+
+
+def hjac_schedule(L, nu1=1, nu2=1, start="a"):
+    """V-cycle of M-FEANet-mg_test.ipynb MultiGrid.Step with mode='hjac' (:27346-27372 with Relax =
+    HJacIterator.HRelax, :147-155): every relaxation is one learned-smoother sweep ("hsweep", l, src,
+    dst; src None = zero guess), so nothing is fused with the transfers:
+    residual + restriction ("resid_restrict" with the current iterate) and prolongation + correction
+    ("prolong_add") run as their own kernels; coarse levels start from zero, the coarsest gets
+    nu1 + nu2 sweeps."""
+    if L < 1 or nu1 < 0 or nu2 < 0:
+        raise ValueError("hjac_schedule: need L >= 1, nu1, nu2 >= 0")
+    steps = []
+    cur = ["zero"] * L
+    cur[0] = start
+
+    def hs(l):
+        dst = "a" if cur[l] == "zero" else _other(cur[l])
+        steps.append(("hsweep", l, None if cur[l] == "zero" else cur[l], dst))
+        cur[l] = dst
+
+    if L == 1:
+        for _ in range(nu1 + nu2):
+            hs(0)
+        return steps, cur[0]
+    for _ in range(nu1):
+        hs(0)
+    for l in range(L - 1):
+        steps.append(("resid_restrict", l, cur[l], None))
+        if l + 1 < L - 1:
+            for _ in range(nu1):
+                hs(l + 1)
+    for _ in range(nu1 + nu2):
+        hs(L - 1)
+    for l in range(L - 2, -1, -1):
+        dst = "a" if cur[l] == "zero" else _other(cur[l])
+        steps.append(("prolong_add", l, cur[l], cur[l + 1], dst))
+        cur[l] = dst
+        for _ in range(nu2):
+            hs(l)
+    return steps, cur[0]

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import vcycle_schedule
+from .schedule import hjac_schedule, vcycle_schedule
 
 
 class _Level:
@@ -92,11 +92,16 @@ class MultigridSolver:
             (fea_mg_sweep_restrict, one read of u and f); False issues them separately.
         zero_start: every V-cycle starts the finest level from a zero guess too (the replicated coarse
             sub-solve of the domain-decomposed path, feanet_amd.dd).
+        smoother: "jac" (weighted Jacobi) or "hjac" (the learned smoother of M-FEANet-mg_test.ipynb,
+            HJacIterator.HRelax: Jacobi + HNet correction; `hnet` = its [nl, 3, 3] conv weights, e.g.
+            feanet_amd/weights/hnet_iso_poisson_33x33.npz).  "hjac" runs fea_mg_hsweep for every
+            relaxation (MultiGrid(mode='hjac').Step semantics) and no coarse tail.
     """
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
-                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False):
+                 nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
+                 smoother="jac", hnet=None):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -127,6 +132,18 @@ class MultigridSolver:
         self.use_graph = graph
         self.fuse = fuse
         self.zero_start = zero_start
+        if smoother not in ("jac", "hjac"):
+            raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
+        self.smoother = smoother
+        if smoother == "hjac":
+            if hnet is None:
+                raise ValueError("MultigridSolver: smoother='hjac' needs the HNet weights (hnet=[nl, 3, 3])")
+            if compat is not None or zero_start:
+                raise ValueError("MultigridSolver: smoother='hjac' follows MultiGrid(mode='hjac').Step only")
+            hw = np.asarray(torch.as_tensor(hnet).detach().cpu().float().numpy(), np.float32).reshape(-1, 3, 3)
+            if not 1 <= hw.shape[0] <= 3:
+                raise ValueError("MultigridSolver: HNet with 1..3 conv layers supported")
+            coarse_tail = False
         npdt = np.float32 if dtype == torch.float32 else np.float64
         multi = problem == "interface"
         if problem not in ("poisson", "interface"):
@@ -149,6 +166,11 @@ class MultigridSolver:
         self.w = (w[0], w[1])
         dev = self.device
         self.ktab_np = ktab
+        self.hw = None
+        self.nl = 0
+        if smoother == "hjac":
+            self.hw = torch.from_numpy(hw.reshape(-1).astype(npdt)).to(dev)
+            self.nl = hw.shape[0]
         self.ktab = torch.from_numpy(ktab.reshape(-1, 9).astype(npdt)).to(dev)
         self.omd = torch.from_numpy(ms.omega_over_d(ktab, omega, npdt)).to(dev)
         self.rtab = torch.from_numpy(np.ascontiguousarray(R).reshape(-1, 9).astype(npdt)).to(dev)
@@ -257,6 +279,13 @@ class MultigridSolver:
         self._pack(u0, L0.a, bc=bc)
         self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
         self._state = "a"
+        if self.smoother == "hjac":
+            # HRelax forms J(u) - u with the iterate the driver passed, before reset_boundary
+            # (M-FEANet-mg_test.ipynb:151-153; the drivers pass un-reset zeros, :27478-27489): the
+            # first sweep of the next V-cycle sees bc - u0 on the boundary nodes
+            self._raw = torch.zeros_like(L0.a)
+            self._pack(u0, self._raw, reset=False)
+            self._hjac_first = True
 
     def solution(self):
         """Current fine iterate as a contiguous [B, 1, H, W] tensor."""
@@ -282,8 +311,11 @@ class MultigridSolver:
     def _build(self, start):
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
-        steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
-                                     top_zero=self.zero_start)
+        if self.smoother == "hjac":
+            steps, end = hjac_schedule(self.L, self.nu1, self.nu2, start)
+        else:
+            steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
+                                         top_zero=self.zero_start)
         return [self.bind_step(st) for st in steps], end
 
     def bind_step(self, st):
@@ -309,6 +341,9 @@ class MultigridSolver:
         f = lv[l].f.data_ptr()
         if kind == "sweep":
             return ("mg_sweep", (ptr(l, st[2]), f, ptr(l, st[3]), pid(l), kt, om, nt) + geom(l))
+        if kind == "hsweep":
+            return ("mg_hsweep", (ptr(l, st[2]), None, f, ptr(l, st[3]), pid(l), kt, om, nt, self.hw.data_ptr(),
+                                  self.nl) + geom(l))
         if kind == "resid_restrict":
             return ("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
                                              kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
@@ -343,6 +378,16 @@ class MultigridSolver:
         """Run k V-cycles on the resident iterate (asynchronous; no host sync)."""
         for _ in range(k):
             plan, end = self._plan(self._state)
+            if getattr(self, "_hjac_first", False):
+                self._hjac_first = False
+                first = list(plan)
+                for i, (name, args) in enumerate(first):
+                    if name == "mg_hsweep" and args[0] == self._ptr(0, self._state):
+                        first[i] = (name, (args[0], self._raw.data_ptr()) + args[2:])
+                        break
+                self._launch(first)
+                self._state = end
+                continue
             if not self.use_graph or self._eager_runs.get(self._state, 0) == 0:
                 self._eager_runs[self._state] = self._eager_runs.get(self._state, 0) + 1
                 self._launch(plan)
