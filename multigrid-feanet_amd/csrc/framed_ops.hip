@@ -44,7 +44,11 @@ static inline int mg_nstrips(int W) { return div_up(W - 2, Frame<T>::SW); }
 template <typename T>
 static inline int mg_ld(int W) {
   using F = Frame<T>;
-  const int need = F::OFF + 2 + std::max(mg_nstrips<T>(W) * F::SW + F::VEC, W + F::SW / 2 + 1);
+  // room for the last strip's loads: plain strips (k * SW + halo) and the overlapped strips of
+  // k_mg_sweep_restrict (start 1 + k*S - VEC, 64*VEC columns), S = ((63*VEC - 3)/VEC)*VEC
+  constexpr int S = ((63 * F::VEC - 3) / F::VEC) * F::VEC;
+  const int ovl = 1 + (div_up(W - 2, S) - 1) * S - F::VEC + F::SW;
+  const int need = F::OFF + 2 + std::max(std::max(mg_nstrips<T>(W) * F::SW + F::VEC, W + F::SW / 2 + 1), ovl);
   return div_up(need, F::A) * F::A;
 }
 
@@ -547,94 +551,42 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
 // Kernel E: fused pre-smooth + residual + restriction on a level with a given iterate
 // (temporal blocking of FEANet/multigrid.py:165 then :168-170):
 //   u' = J(u, f)  (stored, interior)     f_c = w0 R(f - K u')
-// One pass reads u and f once (plus halos) instead of twice.  The residual of a row needs u' at
-// the lane's window columns L..RR; inner lanes get them from neighbours by DPP, the two edge lanes
-// compute u' at their halo columns themselves (lane 0: c0-1; lane 63: c0+SW, c0+SW+1).
+// One pass reads u and f once instead of twice.  OVERLAPPED STRIPS: a wave loads 64*VEC columns
+// starting VEC columns left of the S it owns (S = 122 fp64, 248 fp32) and computes u' and the
+// residual on all of them; the values its two edge lanes get wrong (missing neighbours) are never
+// stored, so there is no edge-lane recomputation and no halo load (5 % of the columns are loaded
+// twice instead).  Rounding is the same per node as every other kernel (fp-contract=on).
 // ---------------------------------------------------------------------------
-template <typename T, int V>
-struct XRaw {  // row load with the extra halo column(s) the edge sweeps need
-  T x[V], h[V], hx;
+template <typename T>
+struct Ovl {
+  static constexpr int V = Frame<T>::VEC;
+  static constexpr int S = ((63 * V - 3) / V) * V;  // owned fine columns per strip (mult. of V)
+  static constexpr int OWN = S / V;                 // owning lanes: 1 .. OWN
 };
-template <int V>
-struct XRawP {
-  int x[V], h[V], hx;
-};
+
 template <typename T, int V>
-struct XRow {
+__device__ __forceinline__ Row<T, V> own_row(const T (&x)[V]) {  // window L, own.., R from own values
   Row<T, V> w;
-  T el, er;  // lane 0: column c0-2; lane 63: column c0+SW+2 (other lanes: unused)
-};
+#pragma unroll
+  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k];
+  w.a[0] = shr1(x[V - 1], T(0));
+  w.a[V + 1] = shl1(x[0], T(0));
+  return w;
+}
 template <int V>
-struct XPRow {
+__device__ __forceinline__ PRow<V> own_prow(const int (&x)[V]) {
   PRow<V> w;
-  int el, er;
-};
-
-template <typename T, int V>
-__device__ __forceinline__ XRaw<T, V> xraw_row(const T* __restrict__ rp, int lane) {
-  XRaw<T, V> r;
-  vload<T, V>(rp + V * lane, r.x);
 #pragma unroll
-  for (int k = 0; k < V; ++k) r.h[k] = T(0);
-  r.hx = T(0);
-  if (lane == 0 || lane == kWave - 1) {
-    vload<T, V>(rp + (lane == 0 ? -V : kWave * V), r.h);
-    if constexpr (V == 2) {
-      if (lane == kWave - 1) r.hx = rp[kWave * V + 2];
-    }
-  }
-  return r;
-}
-template <int V>
-__device__ __forceinline__ XRawP<V> xraw_prow(const uint8_t* __restrict__ pp, int lane) {
-  XRawP<V> r;
-  pload<V>(pp + V * lane, r.x);
-#pragma unroll
-  for (int k = 0; k < V; ++k) r.h[k] = 0;
-  r.hx = 0;
-  if (lane == 0 || lane == kWave - 1) {
-    pload<V>(pp + (lane == 0 ? -V : kWave * V), r.h);
-    if constexpr (V == 2) {
-      if (lane == kWave - 1) r.hx = pp[kWave * V + 2];
-    }
-  }
-  return r;
-}
-template <typename T, int V>
-__device__ __forceinline__ XRow<T, V> xfinish(const XRaw<T, V>& r) {
-  XRow<T, V> o;
-  RawRow<T, V> rr;
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    rr.x[k] = r.x[k];
-    rr.h[k] = r.h[k];
-  }
-  o.w = finish(rr);
-  o.el = r.h[V - 2];                       // lane 0: c0-2
-  o.er = (V == 2) ? r.hx : r.h[2 % V];     // lane 63: c0+SW+2
-  return o;
-}
-template <int V>
-__device__ __forceinline__ XPRow<V> xfinish(const XRawP<V>& r) {
-  XPRow<V> o;
-  RawP<V> rr;
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    rr.x[k] = r.x[k];
-    rr.h[k] = r.h[k];
-  }
-  o.w = finish(rr);
-  o.el = r.h[V - 2] * kTabStride;
-  o.er = ((V == 2) ? r.hx : r.h[2 % V]) * kTabStride;
-  return o;
+  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * kTabStride;
+  w.a[0] = shr1(x[V - 1], 0) * kTabStride;
+  w.a[V + 1] = shl1(x[0], 0) * kTabStride;
+  return w;
 }
 
-#ifndef FEA_SR_WAVES_PER_EU
-#define FEA_SR_WAVES_PER_EU 1  // forcing 3 (168 VGPRs) spills and measured slower (119 vs 107 us)
-#endif
 template <typename T, bool MULTI, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 : FEA_SR_WAVES_PER_EU))) void k_mg_sweep_restrict(MgArgs<T> g) {
+__global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
   using F = Frame<T>;
+  using O = Ovl<T>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
@@ -647,10 +599,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
   if (!id.valid) return;
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
-  const int c0 = 1 + id.s * F::SW;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column
+  const int cs = c0 - V;           // first loaded column (16-byte aligned)
+  const int cl = cs + V * lane;    // lane's first column
   const int I0 = 1 + id.t * (g.rb / 2);
   const int I1 = min(I0 + g.rb / 2, Hc - 1);
-  const int cl = c0 + V * lane;
   T ks[9], rs[9];
   T om = 0;
   if constexpr (!MULTI) {
@@ -662,141 +615,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
     om = g.omd[0];
   }
   const T w0 = g.w;
-  const bool L0 = lane == 0, L63 = lane == kWave - 1;
-  // interior flags of the window columns: j = 0..V+2 (L, own, R, RR) and the edge-sweep centres
-  bool cin[V + 3];
+  bool cin[V];
 #pragma unroll
-  for (int j = 0; j < V + 3; ++j) {
-    const int c = cl + j - 1;
-    cin[j] = c >= 1 && c <= W - 2;
-  }
-  const int ce1 = L0 ? c0 - 1 : c0 + F::SW;  // centre column of edge sweep 1
-  const bool e1in = ce1 >= 1 && ce1 <= W - 2;
-  const bool e2in = c0 + F::SW + 1 <= W - 2;  // edge sweep 2 (lane 63): column c0+SW+1
-  const long long poff = F::OFF + c0;
-  const long long boff = (long long)id.b * g.bs + poff;
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  const bool own = lane >= 1 && lane <= O::OWN;
+  const int J0 = (cl + 1) / 2;  // coarse column of the lane's first (2J-1, 2J, 2J+1) window
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
   const T* __restrict__ ub = g.u + boff;
   const T* __restrict__ fb = g.f + boff;
   T* __restrict__ ob = g.out2 + boff;
-  const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
   const int ld = g.ld;
-  const int bc0 = (c0 + 1) / 2;
-  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + bc0 + Q * lane;
-  const int Jl = bc0 + Q * lane;
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld; };
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * lane; };
 
-  struct RawS {
-    XRaw<T, V> u;
-    RawRow<T, V> f;
-    XRawP<V> p;
+  struct In {  // a raw input row: u and f own values (+ pattern ids)
+    T u[V], f[V];
+    int p[V];
   };
-  struct S {  // one row of the input window
-    XRow<T, V> u;
-    Row<T, V> f;
-    XPRow<V> p;
-  };
-  auto raw_s = [&](int y) {
-    RawS r;
-    r.u = xraw_row<T, V>(ub + rowo(y), lane);
-    r.f = raw_row<T, V>(fb + rowo(y), lane);
-    if constexpr (MULTI) r.p = xraw_prow<V>(pb + rowo(y), lane);
+  auto load = [&](int y) {
+    In r;
+    const long long o = rowo(y);
+    vload<T, V>(ub + o, r.u);
+    vload<T, V>(fb + o, r.f);
+    if constexpr (MULTI) pload<V>(pb + o, r.p);
     return r;
   };
-  auto fin_s = [&](const RawS& r) {
-    S s_;
-    s_.u = xfinish(r.u);
-    s_.f = finish(r.f);
-    if constexpr (MULTI) s_.p = xfinish(r.p);
-    return s_;
+  struct Wn {  // an input row in use: u window, f own, pattern window
+    Row<T, V> u;
+    T f[V];
+    PRow<V> p;
   };
-  // weight of tap d at a node with table offset o
-  auto kw = [&](int o, int d) -> T { return MULTI ? tab[o + d] : ks[d]; };
-  // u' row y (window columns L..RR) from input rows y-1, y, y+1 (a, b, c); boundary rows/cols keep u
-  auto usweep = [&](const S& a, const S& b, const S& c, int y) {
-    Row<T, V> o;
+  auto mk = [&](const In& r) {
+    Wn w;
+    w.u = own_row<T, V>(r.u);
+#pragma unroll
+    for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
+    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    return w;
+  };
+  // u'(y) on the lane's own columns (boundary rows / columns keep u)
+  auto usweep = [&](const Wn& a, const Wn& b, const Wn& c, int y, T (&o)[V]) {
     const bool rin = y >= 1 && y <= H - 2;
-    T own[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const T acc = kapply<T, V, MULTI>(a.u.w, b.u.w, c.u.w, a.p.w, b.p.w, c.p.w, k, ks, tab);
-      const T omk = MULTI ? tab[b.p.w.a[k + 1] + 9] : om;
-      const T v = omk * (b.f.a[k + 1] - acc) + b.u.w.a[k + 1];
-      own[k] = (rin && cin[k + 1]) ? v : b.u.w.a[k + 1];
-    }
-    // edge sweep 1: lane 0 at c0-1 (cols c0-2, c0-1, c0); lane 63 at c0+SW (cols c0+SW-1, +SW, +SW+1)
-    T e1, e2;
-    {
-      const S* rows[3] = {&a, &b, &c};
-      T acc = 0;
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const S& q = *rows[dr];
-        const T vm = L0 ? q.u.el : q.u.w.a[V];
-        const T vc = L0 ? q.u.w.a[0] : q.u.w.a[V + 1];
-        const T vp = L0 ? q.u.w.a[1] : q.u.w.a[V + 2];
-        int om_ = 0, oc = 0, op = 0;
-        if constexpr (MULTI) {
-          om_ = L0 ? q.p.el : q.p.w.a[V];
-          oc = L0 ? q.p.w.a[0] : q.p.w.a[V + 1];
-          op = L0 ? q.p.w.a[1] : q.p.w.a[V + 2];
-        }
-        acc += kw(om_, dr * 3 + 0) * vm;
-        acc += kw(oc, dr * 3 + 1) * vc;
-        acc += kw(op, dr * 3 + 2) * vp;
-      }
-      const T uc = L0 ? b.u.w.a[0] : b.u.w.a[V + 1];
-      const T fc = L0 ? b.f.a[0] : b.f.a[V + 1];
-      const T omc = MULTI ? tab[(L0 ? b.p.w.a[0] : b.p.w.a[V + 1]) + 9] : om;
-      const T v = omc * (fc - acc) + uc;
-      e1 = (rin && e1in) ? v : uc;
-    }
-    {  // edge sweep 2 (meaningful in lane 63): centre c0+SW+1, cols c0+SW .. c0+SW+2
-      const S* rows[3] = {&a, &b, &c};
-      T acc = 0;
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const S& q = *rows[dr];
-        int om_ = 0, oc = 0, op = 0;
-        if constexpr (MULTI) {
-          om_ = q.p.w.a[V + 1];
-          oc = q.p.w.a[V + 2];
-          op = q.p.er;
-        }
-        acc += kw(om_, dr * 3 + 0) * q.u.w.a[V + 1];
-        acc += kw(oc, dr * 3 + 1) * q.u.w.a[V + 2];
-        acc += kw(op, dr * 3 + 2) * q.u.er;
-      }
-      const T uc = b.u.w.a[V + 2];
-      const T omc = MULTI ? tab[b.p.w.a[V + 2] + 9] : om;
-      const T v = omc * (b.f.a[V + 2] - acc) + uc;
-      e2 = (rin && e2in) ? v : uc;
-    }
-#pragma unroll
-    for (int k = 0; k < V; ++k) o.a[k + 1] = own[k];
-    o.a[0] = shr1(own[V - 1], e1);
-    o.a[V + 1] = shl1(own[0], e1);
-    o.a[V + 2] = shl1(own[1 % V], e2);
-    return o;
-  };
-  auto store_u = [&](int y, const Row<T, V>& w) {
-    const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
-    if (own) {
-      T o[V];
-#pragma unroll
-      for (int k = 0; k < V; ++k) o[k] = w.a[k + 1];
-      store_masked<T, V, NT>(ob + rowo(y) + V * lane, o, cl, W);
+      const T acc = kapply<T, V, MULTI>(a.u, b.u, c.u, a.p, b.p, c.p, k, ks, tab);
+      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      const T v = omk * (b.f[k] - acc) + b.u.a[k + 1];
+      o[k] = (rin && cin[k]) ? v : b.u.a[k + 1];
     }
   };
-  const int ya = 2 * I0 - 1;  // first residual row
-  auto resid_p = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const S& pa, const S& pb_,
-                     const S& pc, const S& sy, T (&r)[V + 1]) {
-#pragma unroll
-    for (int k = 0; k <= V; ++k)
-      r[k] = sy.f.a[k + 1] - kapply<T, V, MULTI>(a, b, c, pa.p.w, pb_.p.w, pc.p.w, k, ks, tab);
+  auto store_u = [&](int y, const T (&o)[V]) {
+    const bool ownr = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
+    if (own && ownr) store_masked<T, V, NT>(ob + rowo(y), o, cl, W);
   };
-  // restriction accumulated row by row: a fine residual row with kernel row ky contributes
-  // R[ky][kx] * r[2q + kx] to coarse output q (per fine-node pattern in the MULTI case)
-  auto racc = [&](T (&acc)[Q], const T (&r)[V + 1], const PRow<V>& p, int ky, bool init) {
+  // residual row y (u' windows a, b, c; f and patterns of row y) -> restriction row ky into acc
+  auto racc = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const Wn& sy, const Wn& pa,
+                  const Wn& pc, int ky, T (&acc)[Q], bool init) {
+    T r[V + 1];
+#pragma unroll
+    for (int k = 0; k < V; ++k) r[k] = sy.f[k] - kapply<T, V, MULTI>(a, b, c, pa.p, sy.p, pc.p, k, ks, tab);
+    r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       T t;
@@ -805,56 +684,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MULTI ? 1 :
         t += rs[ky * 3 + 1] * r[2 * q + 1];
         t += rs[ky * 3 + 2] * r[2 * q + 2];
       } else {
-        t = rtb[p.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
-        t += rtb[p.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
-        t += rtb[p.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
+        t = rtb[sy.p.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
+        t += rtb[sy.p.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
+        t += rtb[sy.p.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
       }
       acc[q] = init ? t : acc[q] + t;
     }
   };
-  // input rows ya-2 .. ya+2 first
-  S X0 = fin_s(raw_s(ya - 2)), X1 = fin_s(raw_s(ya - 1)), X2 = fin_s(raw_s(ya)), X3 = fin_s(raw_s(ya + 1));
-  RawS nB = raw_s(ya + 3);  // row 2I0+2, consumed in the first half of the first iteration
-  S X4 = fin_s(raw_s(ya + 2));
-  Row<T, V> Uc = usweep(X1, X2, X3, ya);  // u'(2I0-1)
-  store_u(ya, Uc);
-  Row<T, V> Un = usweep(X2, X3, X4, ya + 1);  // u'(2I0)
-  store_u(ya + 1, Un);
-  T acc[Q];
-  {
-    const Row<T, V> Up = usweep(X0, X1, X2, ya - 1);  // u'(2I0-2)
-    T r[V + 1];
-    resid_p(Up, Uc, Un, X1, X2, X3, X2, r);  // residual row 2I0-1 -> coarse I0 with ky = 0
-    racc(acc, r, X2.p.w, 0, true);
-  }
-  // loop state for coarse row I: acc holds the ky = 0 part (fine row 2I-1); u' rows 2I-1 (Uc), 2I (Un);
-  // input rows 2I-1 (X2), 2I (X3), 2I+1 (X4); raw row 2I+2 (nB) in flight.
-  for (int I = I0; I < I1; ++I) {
-    const RawS m1 = raw_s(2 * I + 3);  // consumed in the second half of this iteration
-    const S X5 = fin_s(nB);            // row 2I+2
-    const Row<T, V> U1 = usweep(X3, X4, X5, 2 * I + 1);
-    store_u(2 * I + 1, U1);
-    T r[V + 1];
-    resid_p(Uc, Un, U1, X2, X3, X4, X3, r);  // residual row 2I
-    racc(acc, r, X3.p.w, 1, false);
-    const RawS m2 = raw_s(2 * I + 4);  // consumed in the first half of the next iteration
-    const S X6 = fin_s(m1);            // row 2I+3
-    const Row<T, V> U2 = usweep(X4, X5, X6, 2 * I + 2);
-    store_u(2 * I + 2, U2);
-    resid_p(Un, U1, U2, X3, X4, X5, X4, r);  // residual row 2I+1: ky = 2 for I, ky = 0 for I+1
-    racc(acc, r, X4.p.w, 2, false);
+  auto store_c = [&](int I, const T (&acc)[Q]) {
     T o[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) o[q] = w0 * acc[q];
-    racc(acc, r, X4.p.w, 0, true);
+    if (!own) return;
     T* cp = cb + (long long)(I + 1) * g.ldc;
-    if (Jl + Q - 1 <= Wc - 2) {
+    if (J0 + Q - 1 <= Wc - 2) {
       vstore<T, Q, NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (Jl + q <= Wc - 2) cp[q] = o[q];
+        if (J0 + q <= Wc - 2) cp[q] = o[q];
     }
+  };
+
+  const int ya = 2 * I0 - 1;  // first residual row
+  Wn X0 = mk(load(ya - 2)), X1 = mk(load(ya - 1)), X2 = mk(load(ya)), X3 = mk(load(ya + 1));
+  In nB = load(ya + 3);  // row 2I0+2, consumed in the first half of the first iteration
+  Wn X4 = mk(load(ya + 2));
+  T o[V];
+  usweep(X0, X1, X2, ya - 1, o);  // u'(ya-1), not stored (row of the task above or boundary)
+  const Row<T, V> Up = own_row<T, V>(o);
+  usweep(X1, X2, X3, ya, o);
+  store_u(ya, o);
+  Row<T, V> Uc = own_row<T, V>(o);
+  usweep(X2, X3, X4, ya + 1, o);
+  store_u(ya + 1, o);
+  Row<T, V> Un = own_row<T, V>(o);
+  T acc[Q];
+  racc(Up, Uc, Un, X2, X1, X3, 0, acc, true);  // residual row ya -> coarse I0, ky = 0
+  // loop state for coarse row I: u' rows 2I-1 (Uc), 2I (Un); input rows 2I-1 (X2), 2I (X3),
+  // 2I+1 (X4); raw row 2I+2 (nB) in flight
+  for (int I = I0; I < I1; ++I) {
+    const In m1 = load(2 * I + 3);  // consumed in the second half of this iteration
+    const Wn X5 = mk(nB);           // row 2I+2
+    usweep(X3, X4, X5, 2 * I + 1, o);
+    store_u(2 * I + 1, o);
+    const Row<T, V> U1 = own_row<T, V>(o);
+    racc(Uc, Un, U1, X3, X2, X4, 1, acc, false);  // residual row 2I
+    const In m2 = load(2 * I + 4);  // consumed in the first half of the next iteration
+    const Wn X6 = mk(m1);           // row 2I+3
+    usweep(X4, X5, X6, 2 * I + 2, o);
+    store_u(2 * I + 2, o);
+    const Row<T, V> U2 = own_row<T, V>(o);
+    racc(Un, U1, U2, X4, X3, X5, 2, acc, false);  // residual row 2I+1: ky = 2 for I ...
+    store_c(I, acc);
+    racc(Un, U1, U2, X4, X3, X5, 0, acc, true);   // ... and ky = 0 for I+1
     Uc = U1;
     Un = U2;
     X2 = X4;
@@ -1184,9 +1067,9 @@ static int target_waves() {
   const char* e = getenv("FEANET_TARGET_WAVES");  // default 2048 = 8 waves per CU
   return e ? std::max(64, atoi(e)) : 2048;
 }
-static inline int pick_rb(int B, int nstrips, int rows) {
+static inline int pick_rb(int B, int nstrips, int rows, int maxrb = kRB) {
   const int tw = target_waves();
-  for (int rb = kRB; rb > 2; rb /= 2)
+  for (int rb = maxrb; rb > 2; rb /= 2)
     if ((long long)B * nstrips * div_up(rows, rb) >= tw) return rb;
   return 2;
 }
@@ -1337,6 +1220,8 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.u = u; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
     g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
     g.bsc = bsc;                                                                                             \
+    g.nstrips = div_up(W - 2, Ovl<T>::S);  /* overlapped strips */                                           \
+    g.rb = pick_rb(B, g.nstrips, H - 2, 2 * kRB);                                                            \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
