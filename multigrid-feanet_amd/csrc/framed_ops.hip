@@ -22,6 +22,8 @@
 
 #include "fea_common.h"
 
+#include <type_traits>
+
 namespace fea {
 
 template <typename T>
@@ -45,10 +47,9 @@ template <typename T>
 static inline int mg_ld(int W) {
   using F = Frame<T>;
   // room for the last strip's loads: plain strips (k * SW + halo) and the overlapped strips of
-  // k_mg_sweep_restrict (start 1 + k*S - VEC, 64*VEC columns), S = ((63*VEC - 3)/VEC)*VEC
-  constexpr int S = ((63 * F::VEC - 3) / F::VEC) * F::VEC;
-  const int ovl = 1 + (div_up(W - 2, S) - 1) * S - F::VEC + F::SW;
-  const int need = F::OFF + 2 + std::max(std::max(mg_nstrips<T>(W) * F::SW + F::VEC, W + F::SW / 2 + 1), ovl);
+  // k_mg_sweep_restrict / k_mg_cycle_join (start <= W - 2, 64*VEC columns)
+  // (any strip starts at a column <= W - 2, so W + 2*SW columns cover every variant's last loads)
+  const int need = F::OFF + 2 + std::max(mg_nstrips<T>(W) * F::SW + F::VEC, W + 2 * F::SW);
   return div_up(need, F::A) * F::A;
 }
 
@@ -230,6 +231,7 @@ struct MgArgs {
   double* part;
   int ntab, nrtab, nptab;
   T w;
+  T w2;  // second ratio (cycle join: w1 of the prolongation)
   int H, W, ld;  // rows, columns of the (local) grid
   long long bs;
   int Hc, Wc, ldc;
@@ -958,6 +960,241 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel F: cycle join — the post-smooth of V-cycle k and the pre-smooth + residual + restriction
+// of V-cycle k+1 on one level in ONE pass (temporal blocking across the cycle boundary):
+//   x = u + w1 P(ec)        (FEANet/multigrid.py:177-180, prolongation + correction)
+//   v = J(x, f)             (:181, post-smooth of cycle k — never stored)
+//   w = J(v, f)             (:165, pre-smooth of cycle k+1 — stored)
+//   f_c = w0 R(f - K w)     (:168-170, restriction of cycle k+1)
+// Reads u, f, ec once and writes w, f_c: 28 instead of 52 B per fine node for the two passes it
+// replaces.  Overlapped strips with a 2*VEC-column left halo (S = 120 fp64 / 244 fp32 owned
+// columns per 64*VEC loaded); a row task streams its rows through the four stages skewed by one
+// row each.  Per-node arithmetic is exactly that of fea_mg_prolong_sweep then fea_mg_sweep_restrict,
+// so the result is bitwise the unfused sequence.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct Ovl3 {
+  static constexpr int V = Frame<T>::VEC;
+  static constexpr int HL = 2 * V;                       // left halo columns (keeps 16-B alignment)
+  static constexpr int S = ((64 * V - 4 - HL) / V) * V;  // owned fine columns per strip
+  static constexpr int L0 = HL / V;                      // first owning lane
+  static constexpr int OWN = S / V;                      // owning lanes L0 .. L0 + OWN - 1
+};
+
+template <typename T, bool MULTI, bool NT>
+__global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
+  using F = Frame<T>;
+  using O = Ovl3<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    load_tables<T>(ptb, g.ptab, nullptr, g.nptab, nullptr, nullptr, 0);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column (odd)
+  const int cs = c0 - O::HL;       // first loaded column (odd)
+  const int cl = cs + V * lane;    // lane's first column (odd)
+  const int I0 = 1 + id.t * (g.rb / 2);
+  const int I1 = min(I0 + g.rb / 2, Hc - 1);
+  T ks[9], rs[9], ps[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      rs[d] = g.rtab[d];
+      ps[d] = g.ptab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w0 = g.w, w1 = g.w2;
+  bool cin[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  const bool own = lane >= O::L0 && lane < O::L0 + O::OWN;
+  const int J0 = (cl + 1) / 2;
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const T* __restrict__ ub = g.u + boff;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ ob = g.out2 + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  const long long cboff = F::OFF + (cs + 1) / 2;  // coarse column of lane 0's first value
+  const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + cboff;
+  const uint8_t* __restrict__ pcb = MULTI ? g.pidc + cboff : nullptr;
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
+  const int ld = g.ld, ldc = g.ldc;
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * lane; };
+  auto crowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc) + 1) * ldc; };
+  auto rc = [&](int a) { return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane); };
+
+  // ---- pipeline state (rows relative to the step's y)
+  Row<T, V> Xa{}, Xb{}, Xc{};  // x windows of rows y-2, y-1, y
+  Row<T, V> Va{}, Vb{}, Vc{};  // v windows of rows y-3, y-2, y-1
+  Row<T, V> Wa{}, Wb{}, Wc_{}; // w windows of rows y-4, y-3, y-2
+  PRow<V> P4{}, P3{}, P2{}, P1{}, P0{};  // pattern windows of rows y-4 .. y
+  T f1[V], f2[V], f3[V];       // f of rows y-1, y-2, y-3
+  T um1[V];                    // u (uncorrected) of row y-1: v keeps it on boundary nodes
+  T acc[Q];
+#pragma unroll
+  for (int k = 0; k < V; ++k) f1[k] = f2[k] = f3[k] = um1[k] = T(0);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) acc[q] = T(0);
+
+  const int ys = 2 * I0 - 4, ye = 2 * I1 + 2;
+  // prefetched inputs of the next step: u(y), f(y-1), pid(y); coarse rows ca = floor(y/2), cbr = ca + 1
+  T nu[V], nf[V];
+  int np[V];
+  vload<T, V>(ub + rowo(ys), nu);
+  vload<T, V>(fb + rowo(ys - 1), nf);
+  if constexpr (MULTI) pload<V>(pb + rowo(ys), np);
+  CRow<T, V> Ca = finish_c<T, V, MULTI>(rc(ys / 2));
+  CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(ys / 2 + 1));
+  RawC<T, V> nC = rc(ys / 2 + 2);
+
+  auto sweep_own = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
+                       const PRow<V>& pb_, const PRow<V>& pc, const T (&fy)[V], const T (&keep)[V], int y,
+                       T (&o)[V]) {
+    const bool rin = y >= 1 && y <= H - 2;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T acck = kapply<T, V, MULTI>(a, b, c, pa, pb_, pc, k, ks, tab);
+      const T omk = MULTI ? tab[pb_.a[k + 1] + 9] : om;
+      const T v = omk * (fy[k] - acck) + b.a[k + 1];
+      o[k] = (rin && cin[k]) ? v : keep[k];
+    }
+  };
+
+  auto step = [&](int y, auto par) {
+    constexpr int ODD = decltype(par)::value;
+    // this step's inputs, next step's loads
+    T u0[V], fy1[V];
+    int p0[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      u0[k] = nu[k];
+      fy1[k] = nf[k];
+      if constexpr (MULTI) p0[k] = np[k];
+    }
+    vload<T, V>(ub + rowo(y + 1), nu);
+    vload<T, V>(fb + rowo(y), nf);
+    if constexpr (MULTI) pload<V>(pb + rowo(y + 1), np);
+    // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
+    T x[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      T t;
+      if constexpr (!ODD) {
+        t = crow_term<T, V, MULTI>(Ca, k + 1, 1, ps, ptb);
+      } else {
+        t = crow_term<T, V, MULTI>(Ca, k + 1, 2, ps, ptb) + crow_term<T, V, MULTI>(Cb, k + 1, 0, ps, ptb);
+      }
+      x[k] = u0[k] + w1 * t;
+    }
+    if constexpr (ODD) {  // next (even) step uses coarse row (y+1)/2 = Cb; prefetch the one after
+      Ca = Cb;
+      Cb = finish_c<T, V, MULTI>(nC);
+      nC = rc((y + 1) / 2 + 2);
+    }
+    Xa = Xb;
+    Xb = Xc;
+    Xc = own_row<T, V>(x);
+    P4 = P3;
+    P3 = P2;
+    P2 = P1;
+    P1 = P0;
+    if constexpr (MULTI) P0 = own_prow<V>(p0);
+    // 2. v(y-1) = J(x) (boundary nodes keep u)
+    if (y >= ys + 2) {
+      T v[V];
+      sweep_own(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - 1, v);
+      Va = Vb;
+      Vb = Vc;
+      Vc = own_row<T, V>(v);
+      // 3. w(y-2) = J(v) (boundary nodes keep v)
+      if (y >= ys + 4) {
+        T keep[V], w[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) keep[k] = Vb.a[k + 1];
+        sweep_own(Va, Vb, Vc, P3, P2, P1, f1, keep, y - 2, w);
+        const int yw = y - 2;
+        const bool ownr = yw >= 2 * I0 - 1 && (yw < 2 * I1 - 1 || I1 == Hc - 1) && yw <= H - 2;
+        if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, W);
+        Wa = Wb;
+        Wb = Wc_;
+        Wc_ = own_row<T, V>(w);
+        // 4. residual row y-3 -> restriction
+        if (y >= ys + 6) {
+          T r[V + 1];
+#pragma unroll
+          for (int k = 0; k < V; ++k) r[k] = f2[k] - kapply<T, V, MULTI>(Wa, Wb, Wc_, P4, P3, P2, k, ks, tab);
+          r[V] = shl1(r[0], T(0));
+          auto term = [&](int q, int ky) -> T {
+            T t;
+            if constexpr (!MULTI) {
+              t = rs[ky * 3 + 0] * r[2 * q];
+              t += rs[ky * 3 + 1] * r[2 * q + 1];
+              t += rs[ky * 3 + 2] * r[2 * q + 2];
+            } else {
+              t = rtb[P3.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
+              t += rtb[P3.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
+              t += rtb[P3.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
+            }
+            return t;
+          };
+          const int yr = y - 3;
+          if constexpr (!ODD) {  // yr odd = 2I+1: ky = 2 closes coarse row I, ky = 0 opens I+1
+            if (yr > 2 * I0 - 1) {
+              const int I = (yr - 1) / 2;
+              T o[Q];
+#pragma unroll
+              for (int q = 0; q < Q; ++q) o[q] = w0 * (acc[q] + term(q, 2));
+              if (own) {
+                T* cp = cb + (long long)(I + 1) * ldc;
+                if (J0 + Q - 1 <= Wc - 2) {
+                  vstore<T, Q, NT>(cp, o);
+                } else {
+#pragma unroll
+                  for (int q = 0; q < Q; ++q)
+                    if (J0 + q <= Wc - 2) cp[q] = o[q];
+                }
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc[q] = term(q, 0);
+          } else {  // yr even = 2I: ky = 1
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc[q] = acc[q] + term(q, 1);
+          }
+        }
+      }
+    }
+    // rotate f and u rows
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      f3[k] = f2[k];
+      f2[k] = f1[k];
+      f1[k] = fy1[k];
+      um1[k] = u0[k];
+    }
+  };
+
+  int y = ys;
+  for (; y < ye; y += 2) {
+    step(y, std::integral_constant<int, 0>{});
+    step(y + 1, std::integral_constant<int, 1>{});
+  }
+  step(y, std::integral_constant<int, 0>{});
+}
+
+// ---------------------------------------------------------------------------
 // Kernel D: per-task partial sums of (f - K u)^2 over the interior (deterministic).
 // ---------------------------------------------------------------------------
 template <typename T, bool MULTI>
@@ -1267,6 +1504,30 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
                                           long long bsc, void* stream) {                                     \
     return mg_prolong_##SUF(u, ec, nullptr, out, nullptr, pidc, nullptr, nullptr, 0, ptab, nptab, w1, B, H,  \
                             W, ld, bs, ldc, bsc, stream, false);                                             \
+  }                                                                                                          \
+  extern "C" int fea_mg_cycle_join_##SUF(const T* u, const T* ec, const T* f, T* u_out, T* fc, const uint8_t* pid, \
+                                         const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab, \
+                                         int nptab, const T* rtab, int nrtab, T w1, T w0, int B, int H, int W,     \
+                                         int ld, long long bs, int ldc, long long bsc, void* stream) {            \
+    if (!u || !ec || !f || !u_out || !fc || !ktab || !omd || !ptab || !rtab || B <= 0 || u_out == u)          \
+      return FEA_EINVAL;                                                                                     \
+    if (!layout_ok<T>(H, W, ld, bs) || !coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                     \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nrtab != ntab && nrtab != 1) || (nptab != ntab && nptab != 1)) \
+      return FEA_EINVAL;                                                                                     \
+    const bool multi = ntab > 1;                                                                             \
+    if (multi && (!pid || !pidc || nrtab == 1 || nptab == 1)) return FEA_EINVAL;                             \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
+    g.u = u; g.ec = ec; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.pidc = pidc; g.ktab = ktab;       \
+    g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;     \
+    g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
+    g.nstrips = div_up(W - 2, Ovl3<T>::S);                                                                   \
+    g.rb = pick_rb(B, g.nstrips, H - 2, 2 * kRB);                                                            \
+    g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (multi) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true)                                                  \
+    else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false)                                                       \
+    FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \
                                             int ntab, double* out, double* ws, int B, int H, int W, int ld,   \

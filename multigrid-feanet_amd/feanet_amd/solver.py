@@ -96,12 +96,15 @@ class MultigridSolver:
             HJacIterator.HRelax: Jacobi + HNet correction; `hnet` = its [nl, 3, 3] conv weights, e.g.
             feanet_amd/weights/hnet_iso_poisson_33x33.npz).  "hjac" runs fea_mg_hsweep for every
             relaxation (MultiGrid(mode='hjac').Step semantics) and no coarse tail.
+        join_cycles: vcycle(k) with k >= 2 runs the finest level's post-smooth of each cycle and the
+            pre-smooth + residual + restriction of the next as one pass (fea_mg_cycle_join; bitwise
+            the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
     """
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None):
+                 smoother="jac", hnet=None, join_cycles=True):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -132,6 +135,7 @@ class MultigridSolver:
         self.use_graph = graph
         self.fuse = fuse
         self.zero_start = zero_start
+        self.join_cycles = join_cycles
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -374,8 +378,60 @@ class MultigridSolver:
         for name, args in plan:
             _lib.call(name, self.dtype, *args, stream)
 
+    def _joinable(self):
+        return (self.join_cycles and self.smoother == "jac" and self.nu1 == 1 and self.nu2 == 1 and
+                self.compat is None and not self.zero_start and self.fuse and self.L >= 2)
+
+    def _join_call(self, pre, ec_ptr):
+        """fea_mg_cycle_join: PS(0) of the cycle whose pre-smoothed iterate is in `pre`, fused with the
+        next cycle's SR(0); the new pre-smoothed iterate lands in the other buffer."""
+        lv = self.levels
+        L0, L1 = lv[0], lv[1]
+        pid = None if L0.pid is None else L0.pid.data_ptr()
+        pidc = None if L1.pid is None else L1.pid.data_ptr()
+        return ("mg_cycle_join", (self._ptr(0, pre), ec_ptr, L0.f.data_ptr(), self._ptr(0, "b" if pre == "a" else "a"),
+                                  L1.f.data_ptr(), pid, pidc, self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab,
+                                  self.ptab.data_ptr(), self.ptab.shape[0], self.rtab.data_ptr(),
+                                  self.rtab.shape[0], self.w[1], self.w[0]) + L0.geom() + (L1.ld, L1.bs))
+
+    def _run_segment(self, key, launches):
+        """Launch a fixed list of calls: eager the first time, then as a captured HIP graph."""
+        if not self.use_graph or self._eager_runs.get(key, 0) == 0:
+            self._eager_runs[key] = self._eager_runs.get(key, 0) + 1
+            self._launch(launches)
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.graph(g, stream=s):
+                self._launch(launches)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._graphs[key] = g
+        g.replay()
+
+    def _vcycles_joined(self, k):
+        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles)."""
+        other = lambda b: "b" if b == "a" else "a"
+        s0 = self._state
+        plan, _ = self._plan(s0)
+        head, mid = plan[0], plan[1:-1]
+        ec_ptr = plan[-1][1][1]  # level-1 correction the finest prolongation reads (same every cycle)
+        self._run_segment(("head", s0), [head])
+        pre = other(s0)
+        for _ in range(k - 1):
+            self._run_segment(("join", pre), mid + [self._join_call(pre, ec_ptr)])
+            pre = other(pre)
+        tail = self._plan(other(pre))[0][-1]  # PS(0): pre -> other(pre)
+        self._run_segment(("tail", pre), mid + [tail])
+        self._state = other(pre)
+
     def vcycle(self, k=1):
         """Run k V-cycles on the resident iterate (asynchronous; no host sync)."""
+        if k >= 2 and self._joinable() and not getattr(self, "_hjac_first", False):
+            self._vcycles_joined(k)
+            return
         for _ in range(k):
             plan, end = self._plan(self._state)
             if getattr(self, "_hjac_first", False):
@@ -429,12 +485,27 @@ class MultigridSolver:
         return self.solution(), hist
 
     # ------------------------------------------------------------------ accounting
-    def bytes_per_vcycle(self):
-        """Algorithmic HBM bytes of one V-cycle as executed (DESIGN.md §4 accounting)."""
+    def bytes_per_vcycle(self, k=1):
+        """Algorithmic HBM bytes per V-cycle of vcycle(k) as executed (DESIGN.md §3 accounting); with
+        joined cycles (k >= 2) the k-1 boundaries run fea_mg_cycle_join instead of PS(0) + SR(0)."""
+        esz = 4 if self.dtype == torch.float32 else 8
+        plan = self._plan(self._state)[0]
+        one = self._plan_bytes(plan)
+        if k < 2 or not self._joinable():
+            return one
+        L0, L1 = self.levels[0], self.levels[1]
+        nodes = L0.B * (L0.H - 2) * (L0.W - 2)
+        coarse = L1.B * (L1.H - 2) * (L1.W - 2)
+        pb = 1 if self.problem == "interface" else 0
+        join = nodes * (3 * esz + pb) + coarse * (2 * esz + pb)
+        edge = self._plan_bytes([plan[0], plan[-1]])  # SR(0) + PS(0) replaced by one join per boundary
+        return (k * one - (k - 1) * edge + (k - 1) * join) / k
+
+    def _plan_bytes(self, plan):
         esz = 4 if self.dtype == torch.float32 else 8
         pb = 1 if self.problem == "interface" else 0
         total = 0
-        for name, args in self._plan(self._state)[0]:
+        for name, args in plan:
             if name == "mg_coarse_tail":
                 continue
             B, H, W = (args[-7:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",

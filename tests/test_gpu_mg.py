@@ -506,3 +506,71 @@ def test_vcycle_rect_vs_oracle(T, m, n, tail):
         np.testing.assert_allclose(s.residual_norm().cpu().numpy(), orc.interior_norm(f - mg_o.levels[0].K(v)),
                                    rtol=1e-9 if T == torch.float64 else 2e-3,
                                    atol=(1e-12 if T == torch.float64 else 1e-6) * r0.max())
+
+
+# ----------------------------------------------------------------------------- cycle join
+@pytest.mark.parametrize("T", [torch.float64, torch.float32])
+@pytest.mark.parametrize("problem,n,m,B", [("poisson", 256, None, 1), ("poisson", 1024, None, 2),
+                                           ("poisson", 128, 512, 1), ("interface", 256, None, 2),
+                                           ("poisson", 4, None, 1), ("poisson", 64, 8, 3)])
+@pytest.mark.parametrize("k", [2, 3, 6])
+def test_cycle_join_bitwise(T, problem, n, m, B, k):
+    """vcycle(k) with the finest level's cycle boundaries joined (fea_mg_cycle_join) is bitwise the
+    unjoined sequence of k V-cycles; the graph-replayed second call as well."""
+    from feanet_amd.solver import MultigridSolver
+    rows = m if m is not None else n
+    rng = np.random.default_rng(n + rows + k)
+    f = torch.from_numpy(rng.standard_normal((B, 1, rows + 1, n + 1))).cuda().to(T)
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, rows + 1, n + 1))).cuda().to(T)
+    out = []
+    for join in (False, True):
+        kw = dict(rows=m) if m is not None else {}
+        s = MultigridSolver(n, problem=problem, dtype=T, batch=B, join_cycles=join, **kw)
+        s.set_rhs(f=f)
+        s.load(u0)
+        s.vcycle(k)
+        a = s.solution()
+        s.vcycle(k)   # second call: segments replayed as graphs
+        out.append((a, s.solution()))
+    assert torch.equal(out[0][0], out[1][0]), (out[0][0] - out[1][0]).abs().max().item()
+    assert torch.equal(out[0][1], out[1][1])
+
+
+def test_cycle_join_kernel_direct():
+    """fea_mg_cycle_join against fea_mg_prolong_sweep + fea_mg_sweep_restrict on random data, including
+    boundary nodes that are not zero (Dirichlet data) and a coarse correction with a nonzero ring."""
+    from feanet_amd import _lib
+    for T in (torch.float64, torch.float32):
+        for (m, n, B, problem) in ((256, 256, 2, "poisson"), (130, 514, 1, "poisson"), (64, 64, 1, "interface")):
+            fr = Frame(n, B, T, problem, m=m)
+            co = Frame(n // 2, B, T, problem, m=m // 2)
+            ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned=(problem == "interface"))
+            nt = ktab.shape[0]
+            rng = np.random.default_rng(m + n)
+            u, f = rand_state(rng, B, (fr.H, fr.W), T)
+            e = rng.standard_normal((B, co.H, co.W)).astype(npdt(T))
+            e[:, 0] = e[:, -1] = 0
+            e[:, :, 0] = e[:, :, -1] = 0
+            for name in ("a", "b"):
+                fr.put(name, u)
+            fr.put("f", f)
+            co.put("a", e)
+            args_ps = (fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), fr.pid(), co.pid(),
+                       kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, 0.75) + fr.args() + (co.L.ld, co.L.bs)
+            _lib.call("mg_prolong_sweep", T, *args_ps, None)
+            # SR from b into a zero-initialised buffer with the same boundary
+            tmp = fr.L.a.clone()
+            _lib.call("mg_sweep_restrict", T, fr.L.b.data_ptr(), fr.L.f.data_ptr(), tmp.data_ptr(), co.L.f.data_ptr(),
+                      fr.pid(), kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *fr.args(), co.L.ld,
+                      co.L.bs, None)
+            ref_u, ref_f = fr.L.view(tmp).clone(), co.get("f").copy()
+            co.put("f", np.zeros_like(ref_f))
+            out = fr.L.a.clone()
+            fr.put("b", u)
+            _lib.call("mg_cycle_join", T, fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.f.data_ptr(), out.data_ptr(),
+                      co.L.f.data_ptr(), fr.pid(), co.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt,
+                      rt.data_ptr(), nt, 0.75, 1.25, *fr.args(), co.L.ld, co.L.bs, None)
+            got_u = fr.L.view(out)
+            assert torch.equal(got_u, ref_u), (T, m, n, (got_u - ref_u).abs().max().item())
+            got_f = co.get("f")
+            assert np.array_equal(got_f[:, 1:-1, 1:-1], ref_f[:, 1:-1, 1:-1]), (T, m, n)
