@@ -106,27 +106,26 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
       }
     return acc;
   };
+  // threads as a 32 x 32 grid over the interior nodes (no per-node integer division)
+  const int tx = tid & 31, ty = tid >> 5;
   auto sweep = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst, bool zero) {
-    const int m = N - 2;
-    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
-      const int r = 1 + q / m, c = 1 + q % m, i = r * N + c;
-      const T om = ktb[P(pk, i) + 9];
-      dst[i] = zero ? om * f[i] : om * (f[i] - Ku(N, pk, src, r, c)) + src[i];
-    }
+    for (int r = 1 + ty; r <= H - 2; r += 32)
+      for (int c = 1 + tx; c <= N - 2; c += 32) {
+        const int i = r * N + c;
+        const T om = ktb[P(pk, i) + 9];
+        dst[i] = zero ? om * f[i] : om * (f[i] - Ku(N, pk, src, r, c)) + src[i];
+      }
     __syncthreads();
   };
   auto residual = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst) {
-    const int m = N - 2;
-    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
-      const int r = 1 + q / m, c = 1 + q % m;
-      dst[r * N + c] = f[r * N + c] - Ku(N, pk, src, r, c);
-    }
+    for (int r = 1 + ty; r <= H - 2; r += 32)
+      for (int c = 1 + tx; c <= N - 2; c += 32) dst[r * N + c] = f[r * N + c] - Ku(N, pk, src, r, c);
     __syncthreads();
   };
   auto restrict_ = [&](int H, int N, const uint8_t* pk, const T* res, T* fc) {  // fine residual -> coarse f
-    const int Nc = (N + 1) / 2, m = Nc - 2, mh = (H + 1) / 2 - 2;
-    for (int q = tid; q < mh * m; q += kTailThreads) {
-      const int I = 1 + q / m, J = 1 + q % m;
+    const int Nc = (N + 1) / 2, Hc = (H + 1) / 2;
+    for (int I = 1 + ty; I <= Hc - 2; I += 32)
+      for (int J = 1 + tx; J <= Nc - 2; J += 32) {
       T acc = 0;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky)
@@ -140,19 +139,19 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     __syncthreads();
   };
   auto prolong_add = [&](int H, int N, const uint8_t* pkc, T* v, const T* e) {  // v += w1 P e, interior
-    const int Nc = (N + 1) / 2, m = N - 2;
-    for (int q = tid; q < (H - 2) * m; q += kTailThreads) {
-      const int y = 1 + q / m, x = 1 + q % m;
+    const int Nc = (N + 1) / 2;
+    for (int y = 1 + ty; y <= H - 2; y += 32)
+      for (int x = 1 + tx; x <= N - 2; x += 32) {
       T acc = 0;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
-        const int ty = y + 1 - ky;
-        if (ty & 1) continue;
+        const int cy = y + 1 - ky;
+        if (cy & 1) continue;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-          const int tx = x + 1 - kx;
-          if (tx & 1) continue;
-          const int j = (ty >> 1) * Nc + (tx >> 1);
+          const int cx = x + 1 - kx;
+          if (cx & 1) continue;
+          const int j = (cy >> 1) * Nc + (cx >> 1);
           acc += ptb[P(pkc, j) + ky * 3 + kx] * e[j];
         }
       }
