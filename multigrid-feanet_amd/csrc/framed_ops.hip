@@ -1318,6 +1318,13 @@ static long long nt_bytes() {
   return e ? atoll(e) : (32ll << 20);
 }
 
+// rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
+static int join_max_rb() {
+  const char* e = getenv("FEANET_JOIN_RB");
+  const int v = e ? atoi(e) : 64;
+  return (v >= 4 && (v & (v - 1)) == 0) ? v : 64;
+}
+
 template <typename T>
 static MgArgs<T> mg_args(int H, int W, int ld, long long bs, int B) {
   MgArgs<T> g{};
@@ -1521,7 +1528,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;     \
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     g.nstrips = div_up(W - 2, Ovl3<T>::S);                                                                   \
-    g.rb = pick_rb(B, g.nstrips, H - 2, 2 * kRB);                                                            \
+    g.rb = pick_rb(B, g.nstrips, H - 2, join_max_rb());                                                      \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \

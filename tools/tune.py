@@ -13,6 +13,7 @@ SETS = {
            "nt_8M": ({}, {"FEANET_NT_BYTES": str(8 << 20)}), "nt_all": ({}, {"FEANET_NT_BYTES": "0"})},
     "tw": {f"tw{t}": ({}, {"FEANET_TARGET_WAVES": str(t)}) for t in (1024, 2048, 4096, 8192)},
     "fuse": {"fuse": ({}, {}), "nofuse": (dict(fuse=False), {}), "notail": (dict(coarse_tail=False), {})},
+    "joinrb": {f"jrb{r}": ({}, {"FEANET_JOIN_RB": str(r)}) for r in (32, 64, 128, 256)},
 }
 
 
