@@ -1,0 +1,120 @@
+"""BASELINE.json configurations as GPU parity cases: each checked against the oracle or
+against the single-GPU path, at the configuration's own size.
+  C2  1025^2 Poisson fp64, 6-level V-cycle                      -> oracle, every cycle, 1e-10
+  C3  2049^2 two-material, learned R/P ratio (multigrid.py)     -> oracle first cycle + convergence
+  C4  8193^2 Poisson fp64 over 8 row slabs (domain decomposed)  -> bitwise the single-GPU V-cycle
+  C5  256 x 1025^2 fp32 batch                                   -> bitwise per-sample independence
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import feanet_oracle as orc
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_c2_1025_six_levels_vs_oracle():
+    from feanet_amd.solver import MultigridSolver
+    n, L = 1024, 6
+    rng = np.random.default_rng(2)
+    f = rng.standard_normal((1, n + 1, n + 1))
+    mg = orc.OracleMultigrid(n, "poisson", np.float64, levels=L)
+    s = MultigridSolver(n, levels=L, dtype=torch.float64)
+    s.set_rhs(f=torch.from_numpy(f).cuda().reshape(1, 1, n + 1, n + 1))
+    s.load()
+    v = np.zeros_like(f)
+    for k in range(3):
+        s.vcycle()
+        v = mg.step(v, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        assert np.abs(got - v).max() / np.abs(v).max() < 1e-10, k
+    # Q3: a 6-level cycle whose coarsest grid (33^2) gets 2 sweeps converges slowly but steadily
+    r = [float(s.residual_norm()[0])]
+    s.vcycle(4)
+    r.append(float(s.residual_norm()[0]))
+    assert r[1] < r[0]
+
+
+def test_c3_2049_interface_learned_ratio():
+    from feanet_amd import mesh_setup as ms
+    from feanet_amd.solver import MultigridSolver
+    w = np.load(os.path.join(HERE, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
+    n = 2048
+    s = MultigridSolver(n, problem="interface", dtype=torch.float64, R=w["R"][0], P=w["P"][:, 0], w=w["w"])
+    F = torch.ones(1, 1, n + 1, n + 1, device="cuda", dtype=torch.float64)
+    s.set_rhs(F=F)
+    s.load()
+    r0 = float(s.residual_norm()[0])
+    s.vcycle()
+    got = s.solution().cpu().numpy()[:, 0]
+    # oracle: same operators; pattern maps from the vectorised builder (bit-exact with the reference's
+    # loop at every size the reference can build, tests/test_setup.py)
+    mg = orc.OracleMultigrid(256, "poisson", np.float64)  # placeholder hierarchy, levels replaced below
+    mg.levels = []
+    ktab = ms.stencil_table((1, 20))
+    for l in range(s.L):
+        lv = orc.Level(n >> l, "poisson", np.float64)
+        lv.ktab = ktab
+        lv.pid = ms.interface_pattern_map((n >> l) + 1)
+        mg.levels.append(lv)
+    mg.L = s.L
+    mg.rtab = np.broadcast_to(np.asarray(w["R"][0], np.float32), (16, 3, 3))
+    mg.ptab = np.asarray(w["P"][:, 0], np.float32)
+    mg.w = tuple(float(x) for x in w["w"])
+    f = orc.conv3x3(np.ones((1, n + 1, n + 1)), orc.fnet_stencil(2.0 / n))
+    v = mg.step(np.zeros((1, n + 1, n + 1)), f)
+    assert np.abs(got - v).max() / np.abs(v).max() < 1e-10
+    # converges monotonically; slowly at this size (contrast 20, and the reference's coarsest level is
+    # two Jacobi sweeps on 3^2): measured 0.76 per cycle here
+    r = [float(s.residual_norm()[0])]
+    for _ in range(15):
+        s.vcycle()
+        r.append(float(s.residual_norm()[0]))
+    assert all(b < a for a, b in zip(r, r[1:])), r
+    assert r[-1] / r0 < 0.05, r
+
+
+def test_c4_8193_dd_eight_slabs_bitwise():
+    from feanet_amd.dd import LocalGroup
+    from feanet_amd.solver import MultigridSolver
+    n = 8192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    f = torch.randn(1, 1, n + 1, n + 1, device="cuda", dtype=torch.float64, generator=g)
+    s = MultigridSolver(n, dtype=torch.float64)
+    s.set_rhs(f=f)
+    s.load()
+    grp = LocalGroup(n, n, 8)
+    grp.set_rhs(f)
+    grp.load()
+    for k in range(2):
+        s.vcycle()
+        grp.vcycle()
+        assert torch.equal(grp.solution(), s.solution()), k
+    torch.testing.assert_close(grp.residual_norm(), s.residual_norm(), rtol=1e-12, atol=0)
+
+
+def test_c5_batch256_1025_fp32():
+    from feanet_amd.solver import MultigridSolver
+    n, B = 1024, 256
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    f = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=torch.float32, generator=g)
+    s = MultigridSolver(n, dtype=torch.float32, batch=B)
+    s.set_rhs(f=f)
+    s.load()
+    r0 = s.residual_norm()
+    s.vcycle(3)
+    ub = s.solution()
+    r3 = s.residual_norm()
+    assert bool((r3 < 0.1 * r0).all())
+    for b in (0, 97, 255):
+        s1 = MultigridSolver(n, dtype=torch.float32, batch=1)
+        s1.set_rhs(f=f[b:b + 1])
+        s1.load()
+        s1.vcycle(3)
+        assert torch.equal(s1.solution()[0], ub[b]), b
