@@ -27,7 +27,8 @@ from . import _lib
 from .schedule import vcycle_schedule
 from .solver import MultigridSolver
 
-DEPTH = 3  # rows per halo exchange
+DEPTH = 3   # rows per halo exchange (f and corrections)
+DEPTH0 = 4  # rows per exchange of the finest iterate (the cycle join reaches 4 rows: x -> v -> w -> r)
 
 
 def global_levels(m, n):
@@ -42,7 +43,7 @@ def default_agglomeration(m, n, P, L, max_nodes=1 << 20):
     """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows."""
     Ld = 1
     while Ld < L - 1 and ((m >> Ld) + 1) * ((n >> Ld) + 1) > max_nodes and m % (P << (Ld + 1)) == 0 \
-            and m // (P << (Ld + 1)) >= 2:
+            and m // (P << (Ld + 1)) >= 4:
         Ld += 1
     return Ld
 
@@ -61,12 +62,12 @@ class LevelPart:
 
 
 class Partition:
-    def __init__(self, m, n, P, Ld, G=2):
+    def __init__(self, m, n, P, Ld, G=4):
         if P < 1 or Ld < 1:
             raise ValueError("Partition: need P >= 1 and Ld >= 1")
-        if m % (P << Ld) or m // (P << Ld) < 2:
+        if m % (P << Ld) or m // (P << Ld) < G:
             raise ValueError(f"Partition: {m} rows do not split into {P} slabs over {Ld} levels "
-                             f"(need m divisible by P*2^Ld with >= 2 coarse rows per rank)")
+                             f"(need m divisible by P*2^Ld with >= {G} coarse rows per rank)")
         if n % (1 << Ld) or (n >> Ld) < 2:
             raise ValueError(f"Partition: {n} columns do not coarsen {Ld} times")
         self.m, self.n, self.P, self.Ld, self.G = m, n, P, Ld, G
@@ -91,7 +92,7 @@ class Partition:
 
 def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a"):
     """The distributed part of one V-cycle (levels 0..Ld-1) with its communication steps:
-    kernel steps of feanet_amd.schedule plus ("exchange", l, buf), ("gather",), ("coarse",),
+    kernel steps of feanet_amd.schedule plus ("exchange", l, buf, depth), ("gather",), ("coarse",),
     ("scatter", dst)."""
     steps, end = vcycle_schedule(Ld + 1, nu1, nu2, None, start, tail_from=Ld, fuse=fuse)
     out = []
@@ -101,12 +102,15 @@ def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a"):
             out += [("gather",), ("coarse",), ("scatter", st[2])]
             continue
         out.append(st)
+        d = DEPTH0 if l == 0 else DEPTH
         if kind == "sweep":
-            out.append(("exchange", l, st[3]))
+            out.append(("exchange", l, st[3], d))
         elif kind in ("prolong_sweep", "prolong_add"):
-            out.append(("exchange", l, st[4]))
-        elif kind in ("resid_restrict", "sweep_restrict") and l + 1 < Ld:
-            out.append(("exchange", l + 1, "f"))
+            out.append(("exchange", l, st[4], d))
+        elif kind == "sweep_restrict":
+            out.append(("exchange", l, st[3], d))  # the pre-smoothed iterate: read by a later cycle join
+        if kind in ("resid_restrict", "sweep_restrict") and l + 1 < Ld:
+            out.append(("exchange", l + 1, "f", DEPTH))
     return out, end
 
 
@@ -207,36 +211,100 @@ class DDSolver:
         return loc.norm_out * loc.norm_out
 
     # ------------------------------------------------------------------ plan
-    def segments(self, start):
-        """One V-cycle as [("k", [(name, args), ...]) | ("c", comm step)], and the end buffer."""
-        if start not in self._segs:
-            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, start)
-            segs = []
-            for st in steps:
-                if st[0] in ("exchange", "gather", "scatter"):
-                    segs.append(("c", st))
-                    continue
-                launches = list(self.coarse_plan) if st[0] == "coarse" else [self.local.bind_step(st)]
-                if segs and segs[-1][0] == "k":
-                    segs[-1][1].extend(launches)
-                else:
-                    segs.append(("k", launches))
-            self._segs[start] = (segs, end)
-        return self._segs[start]
+    def _segs_of(self, steps, launches_extra=None):
+        """Kernel steps -> [("k", launches) | ("c", comm step)] with consecutive kernels merged."""
+        segs = []
+        for st in steps:
+            if st[0] in ("exchange", "gather", "scatter"):
+                segs.append(("c", st))
+                continue
+            if st[0] == "coarse":
+                launches = list(self.coarse_plan)
+            elif st[0] == "join":
+                launches = [self.local._join_call(st[1], st[2])]
+            else:
+                launches = [self.local.bind_step(st)]
+            if segs and segs[-1][0] == "k":
+                segs[-1][1].extend(launches)
+            else:
+                segs.append(("k", launches))
+        return segs
 
-    def run_kernels(self, start, i):
-        """Kernel segment i of the cycle starting in `start` (graph-replayed after its first run)."""
-        segs, _ = self.segments(start)
+    def joinable(self):
+        return self.local._joinable()
+
+    def chunk(self, key):
+        """Cached launch/communication segments of one program chunk:
+        ("cycle", s): a whole V-cycle from buffer s;  ("head", s): its first step (SR(0)) and exchanges;
+        ("join", pre): the rest of a cycle whose pre-smoothed iterate is in `pre`, ending in the cycle
+        join into the other buffer;  ("tail", pre): the same ending in the last PS(0)."""
+        if key in self._segs:
+            return self._segs[key]
+        kind, b = key
+        other = lambda x: "b" if x == "a" else "a"
+        if kind == "cycle":
+            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, b)
+            res = (self._segs_of(steps), end)
+        else:
+            s0 = b if kind == "head" else other(b)  # the start buffer of the cycle the chunk belongs to
+            steps, _ = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, s0)
+            # [SR(0), exch u0, exch f1] + mid + [PS(0), exch u0]
+            i_mid = 1
+            while steps[i_mid][0] == "exchange":
+                i_mid += 1
+            ps0 = max(i for i, st in enumerate(steps) if st[0] == "prolong_sweep" and st[1] == 0)
+            head, mid = steps[:i_mid], steps[i_mid:ps0]
+            if kind == "head":
+                res = (self._segs_of(head), other(b))
+            else:
+                pre = b
+                ec = self.local.bind_step(steps[ps0])[1][1]
+                if kind == "join":
+                    last = [("join", pre, ec), ("exchange", 0, other(pre), DEPTH0)]
+                    if self.Ld > 1:
+                        last.append(("exchange", 1, "f", DEPTH))
+                else:
+                    _, tail_steps = None, dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, other(pre))[0]
+                    ps = [st for st in tail_steps if st[0] == "prolong_sweep" and st[1] == 0][-1]
+                    last = [ps, ("exchange", 0, ps[4], DEPTH0)]
+                res = (self._segs_of(mid + last), other(pre))
+        self._segs[key] = res
+        return res
+
+    def program(self, k):
+        """The chunks of vcycle(k) from the current state, and the end state."""
+        s = self._state
+        if k >= 2 and self.joinable():
+            keys = [("head", s)]
+            pre = "b" if s == "a" else "a"
+            for _ in range(k - 1):
+                keys.append(("join", pre))
+                pre = "b" if pre == "a" else "a"
+            keys.append(("tail", pre))
+            return keys, ("b" if pre == "a" else "a")
+        keys = []
+        for _ in range(k):
+            keys.append(("cycle", s))
+            s = self.chunk(("cycle", s))[1]
+        return keys, s
+
+    def segments(self, start):
+        """One unjoined V-cycle (kept for callers/tests): (segments, end buffer)."""
+        return self.chunk(("cycle", start))
+
+    def run_kernels(self, key, i):
+        """Kernel segment i of chunk `key` (graph-replayed after its first run)."""
+        segs, _ = self.chunk(key)
         launches = segs[i][1]
-        key = (start, i)
+        gkey = (key, i)
         stream = torch.cuda.current_stream(self.device)
-        if not self.use_graph or key not in self._graphs:
+        if not self.use_graph or gkey not in self._graphs:
             if self.use_graph:
-                self._graphs[key] = None  # eager once, capture on the second use
+                self._graphs[gkey] = None  # eager once, capture on the second use
             for name, args in launches:
                 _lib.call(name, self.dtype, *args, stream.cuda_stream)
             return
-        g = self._graphs[key]
+        g = self._graphs[gkey]
         if g is None:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
@@ -245,7 +313,7 @@ class DDSolver:
                 for name, args in launches:
                     _lib.call(name, self.dtype, *args, s.cuda_stream)
             stream.wait_stream(s)
-            self._graphs[key] = g
+            self._graphs[gkey] = g
         g.replay()
 
     # buffers the communication steps touch
@@ -276,18 +344,19 @@ class DDSolver:
     def vcycle(self, k=1):
         if self.comm is None:
             raise RuntimeError("DDSolver.vcycle: no communicator (use LocalGroup for in-process ranks)")
-        for _ in range(k):
-            segs, end = self.segments(self._state)
+        keys, end = self.program(k)
+        for key in keys:
+            segs, _ = self.chunk(key)
             for i, (kind, st) in enumerate(segs):
                 if kind == "k":
-                    self.run_kernels(self._state, i)
+                    self.run_kernels(key, i)
                 elif st[0] == "exchange":
-                    self.comm.exchange(self, st[1], st[2])
+                    self.comm.exchange(self, st[1], st[2], st[3])
                 elif st[0] == "gather":
                     self.comm.allgather(self.gather_target(), self.gather_source())
                 elif st[0] == "scatter":
                     self.scatter(st[1])
-            self._state = end
+        self._state = end
 
     def residual_norm(self):
         n2 = self.residual_norm_sq_local()
@@ -320,17 +389,16 @@ class TorchComm:
     def _stage(self, t):
         return t.contiguous() if self.gpu else t.cpu()
 
-    def exchange(self, s, l, name):
-        """Refresh DEPTH ghost rows on both sides of rank s's slab of level l buffer `name`.  The
-        P2P op lists are built once per (level, buffer) and reused (fixed device views)."""
+    def exchange(self, s, l, name, d=DEPTH):
+        """Refresh d ghost rows on both sides of rank s's slab of level l buffer `name`.  The
+        P2P op lists are built once per (level, buffer, depth) and reused (fixed device views)."""
         dist = self.dist
-        key = (id(s), l, name)
+        key = (id(s), l, name, d)
         plan = self._plans.get(key) if hasattr(self, "_plans") else None
         if plan is None:
             if not hasattr(self, "_plans"):
                 self._plans = {}
             lp = s.parts[l]
-            d = DEPTH
             sends, recvs = [], []
             if s.rank > 0:
                 sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
@@ -399,16 +467,17 @@ class LocalGroup:
             s.load(u0, bc)
 
     def vcycle(self, k=1):
-        for _ in range(k):
-            start = self.ranks[0]._state
-            segs, end = self.ranks[0].segments(start)
+        r0 = self.ranks[0]
+        keys, end = r0.program(k)
+        for key in keys:
+            segs, _ = r0.chunk(key)
             for i, (kind, st) in enumerate(segs):
                 if kind == "k":
                     for s in self.ranks:
-                        s.segments(start)
-                        s.run_kernels(start, i)
+                        s.chunk(key)
+                        s.run_kernels(key, i)
                 elif st[0] == "exchange":
-                    self._exchange(st[1], st[2])
+                    self._exchange(st[1], st[2], st[3])
                 elif st[0] == "gather":
                     chunks = [s.gather_source() for s in self.ranks]
                     for s in self.ranks:
@@ -419,11 +488,10 @@ class LocalGroup:
                 elif st[0] == "scatter":
                     for s in self.ranks:
                         s.scatter(st[1])
-            for s in self.ranks:
-                s._state = end
+        for s in self.ranks:
+            s._state = end
 
-    def _exchange(self, l, name):
-        d = DEPTH
+    def _exchange(self, l, name, d=DEPTH):
         for r, s in enumerate(self.ranks):
             lp = s.parts[l]
             if r > 0:

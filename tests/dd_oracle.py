@@ -101,7 +101,7 @@ def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2):
     """Process entry: one rank of the oracle DD V-cycle over gloo; saves its owned rows."""
     import torch
     import torch.distributed as dist
-    from feanet_amd.dd import DEPTH, dd_schedule
+    from feanet_amd.dd import dd_schedule
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     B = 2
     f, u = problem(m, n, B)
@@ -111,7 +111,7 @@ def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2):
         steps, end = dd_schedule(Ld, 1, 1, True, state)
         for st in steps:
             if st[0] == "exchange":
-                l, name = st[1], st[2]
+                l, name, DEPTH = st[1], st[2], st[3]
                 lp = R.parts[l]
                 ops, recv = [], []
                 if rank > 0:

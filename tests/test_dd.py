@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from feanet_amd.dd import DEPTH, Partition, dd_schedule, default_agglomeration, global_levels
+from feanet_amd.dd import DEPTH, DEPTH0, Partition, dd_schedule, default_agglomeration, global_levels
 from oracle import feanet_oracle as orc
 
 
@@ -29,10 +29,11 @@ def test_partition_invariants(m, n, P, Ld):
                 assert p.gr0 == 2 * q.gr0 and p.Hloc == 2 * q.Hloc - 1  # fine (2I-1, 2I) <-> coarse I locally
                 assert p.s == 2 * q.s - 1  # coarse row I owned with its fine rows (2I-1, 2I)
                 assert p.e == (2 * q.e - 1 if r < P - 1 else H - 1)
+                d = DEPTH0 if l == 0 else DEPTH
                 if r > 0:
-                    assert p.lo >= DEPTH + 1  # exchanged rows + one kept edge row
+                    assert p.lo >= d + 1  # exchanged rows + one kept edge row
                 if r < P - 1:
-                    assert p.Hloc - p.hi >= DEPTH + 1
+                    assert p.Hloc - p.hi >= d + 1
                 assert p.e - p.s >= DEPTH
         assert owned == list(range(1, H - 1)), "interior rows owned exactly once"
 
@@ -42,13 +43,16 @@ def test_partition_rejects_bad_splits():
         Partition(100, 64, 3, 2)
     with pytest.raises(ValueError):
         Partition(64, 64, 8, 3)  # 1 coarse row per rank
+    with pytest.raises(ValueError):
+        Partition(64, 64, 4, 3)  # 2 coarse rows per rank < 4 ghost rows
+    assert Partition(512, 512, 4, 2).ghost(0) == 16
 
 
 def test_dd_schedule_comm_counts():
     for Ld in (1, 2, 3, 5):
         steps, end = dd_schedule(Ld)
         kinds = [s[0] for s in steps]
-        assert kinds.count("exchange") == 2 * Ld - 1
+        assert kinds.count("exchange") == 2 * Ld - 1 + 1  # + the pre-smoothed iterate (read by a join)
         assert kinds.count("gather") == kinds.count("coarse") == kinds.count("scatter") == 1
         assert end in ("a", "b")
 

@@ -54,6 +54,13 @@ def test_dd_local_group_bitwise(m, n, P, Ld, B, graph):
         assert torch.equal(got, ref[k][0]), f"cycle {k}: max diff {(got - ref[k][0]).abs().max().item():.3e}"
         nr = grp.residual_norm()
         torch.testing.assert_close(nr, ref[k][1], rtol=1e-12, atol=0)
+    # several cycles per call: the finest level's cycle boundaries joined on every slab
+    s.vcycle(3)
+    grp.vcycle(3)
+    assert torch.equal(grp.solution(), s.solution())
+    s.vcycle(2)
+    grp.vcycle(2)
+    assert torch.equal(grp.solution(), s.solution())
 
 
 def _free_port():
