@@ -215,7 +215,13 @@ class DDSolver:
         """Kernel steps -> [("k", launches) | ("c", comm step)] with consecutive kernels merged."""
         segs = []
         for st in steps:
-            if st[0] in ("exchange", "gather", "scatter"):
+            if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
+                if segs and segs[-1][0] == "c" and segs[-1][1][0] == "exchanges":
+                    segs[-1][1][1].append(st[1:])
+                else:
+                    segs.append(("c", ("exchanges", [st[1:]])))
+                continue
+            if st[0] in ("gather", "scatter"):
                 segs.append(("c", st))
                 continue
             if st[0] == "coarse":
@@ -350,8 +356,8 @@ class DDSolver:
             for i, (kind, st) in enumerate(segs):
                 if kind == "k":
                     self.run_kernels(key, i)
-                elif st[0] == "exchange":
-                    self.comm.exchange(self, st[1], st[2], st[3])
+                elif st[0] == "exchanges":
+                    self.comm.exchange_many(self, st[1])
                 elif st[0] == "gather":
                     self.comm.allgather(self.gather_target(), self.gather_source())
                 elif st[0] == "scatter":
@@ -390,22 +396,27 @@ class TorchComm:
         return t.contiguous() if self.gpu else t.cpu()
 
     def exchange(self, s, l, name, d=DEPTH):
-        """Refresh d ghost rows on both sides of rank s's slab of level l buffer `name`.  The
-        P2P op lists are built once per (level, buffer, depth) and reused (fixed device views)."""
+        self.exchange_many(s, [(l, name, d)])
+
+    def exchange_many(self, s, items):
+        """Refresh d ghost rows on both sides of rank s's slab for every (level, buffer, d) in `items`,
+        as ONE batch of P2P ops.  The op lists are built once per item list and reused (fixed device
+        views)."""
         dist = self.dist
-        key = (id(s), l, name, d)
+        key = (id(s), tuple(items))
         plan = self._plans.get(key) if hasattr(self, "_plans") else None
         if plan is None:
             if not hasattr(self, "_plans"):
                 self._plans = {}
-            lp = s.parts[l]
             sends, recvs = [], []
-            if s.rank > 0:
-                sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
-                recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
-            if s.rank < s.P - 1:
-                sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
-                recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
+            for l, name, d in items:
+                lp = s.parts[l]
+                if s.rank > 0:
+                    sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
+                    recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
+                if s.rank < s.P - 1:
+                    sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
+                    recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
             direct = self.gpu and all(t.is_contiguous() for t, _ in sends + recvs)
             if direct:
                 sb = [t for t, _ in sends]
@@ -476,8 +487,9 @@ class LocalGroup:
                     for s in self.ranks:
                         s.chunk(key)
                         s.run_kernels(key, i)
-                elif st[0] == "exchange":
-                    self._exchange(st[1], st[2], st[3])
+                elif st[0] == "exchanges":
+                    for l, name, d in st[1]:
+                        self._exchange(l, name, d)
                 elif st[0] == "gather":
                     chunks = [s.gather_source() for s in self.ranks]
                     for s in self.ranks:
