@@ -114,6 +114,16 @@ def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a"):
     return out, end
 
 
+def _launch_list(launches, dtype, stream):
+    """C-ABI calls and ("copy", (dst, src)) device copies, in order, on `stream`."""
+    for name, args in launches:
+        if name == "copy":
+            with torch.cuda.stream(stream):
+                args[0].copy_(args[1])
+        else:
+            _lib.call(name, dtype, *args, stream.cuda_stream)
+
+
 def _rows(t, B, bs, ld, y0, y1):
     """[B, (y1-y0)*ld] view of local rows y0..y1-1 of a framed buffer."""
     return t.as_strided((B, (y1 - y0) * ld), (bs, 1), t.storage_offset() + (y0 + 1) * ld)
@@ -211,20 +221,29 @@ class DDSolver:
         return loc.norm_out * loc.norm_out
 
     # ------------------------------------------------------------------ plan
-    def _segs_of(self, steps, launches_extra=None):
+    def _segs_of(self, steps):
         """Kernel steps -> [("k", launches) | ("c", comm step)] with consecutive kernels merged."""
         segs = []
         for st in steps:
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
+                if self.P == 1:
+                    continue  # no neighbours
                 if segs and segs[-1][0] == "c" and segs[-1][1][0] == "exchanges":
                     segs[-1][1][1].append(st[1:])
                 else:
                     segs.append(("c", ("exchanges", [st[1:]])))
                 continue
-            if st[0] in ("gather", "scatter"):
+            if st[0] == "gather" and self.P > 1:
                 segs.append(("c", st))
                 continue
-            if st[0] == "coarse":
+            if st[0] == "gather":  # one rank: the all-gather is a device copy
+                launches = [("copy", (self.gather_target(), self.gather_source()))]
+            elif st[0] == "scatter":  # a device copy, captured with the kernels around it
+                pl = self.parts[self.Ld]
+                Lc = self.coarse.levels[0]
+                src = _rows(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc)
+                launches = [("copy", (self.level_rows(self.Ld, st[1], 0, pl.Hloc), src))]
+            elif st[0] == "coarse":
                 launches = list(self.coarse_plan)
             elif st[0] == "join":
                 launches = [self.local._join_call(st[1], st[2])]
@@ -307,17 +326,22 @@ class DDSolver:
         if not self.use_graph or gkey not in self._graphs:
             if self.use_graph:
                 self._graphs[gkey] = None  # eager once, capture on the second use
-            for name, args in launches:
-                _lib.call(name, self.dtype, *args, stream.cuda_stream)
+            _launch_list(launches, self.dtype, stream)
             return
         g = self._graphs[gkey]
         if g is None:
+            # thread-local capture: the communicator's own threads (the NCCL watchdog) keep running
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(stream)
-            with torch.cuda.graph(g, stream=s):
-                for name, args in launches:
-                    _lib.call(name, self.dtype, *args, s.cuda_stream)
+            try:
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    _launch_list(launches, self.dtype, s)
+            except RuntimeError:  # capture refused: this rank keeps launching eagerly
+                torch.cuda.synchronize(self.device)
+                self.use_graph = False
+                _launch_list(launches, self.dtype, stream)
+                return
             stream.wait_stream(s)
             self._graphs[gkey] = g
         g.replay()
