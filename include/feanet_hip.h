@@ -123,6 +123,46 @@ int fea_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, co
 int fea_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
                           double* out, double* ws, int B, int H, int W, void* stream);
 
+/* Adjoints of the generic ops, for autograd through the reference's training forward
+ * (MultiGrid.forward / qm, FEANet/multigrid.py:132-157; the reference gets them from torch's
+ * conv2d / conv_transpose2d backward).  Same layouts and argument meaning as the forward ops;
+ * g is the gradient of the forward op's output.
+ *   knet_apply_adj:   out = K^T g                 ((K^T g)[j] = sum_d ktab[pid(j)][d] g[j - d])
+ *   jacobi_sweep_adj: gf = omd . geo . g,  gu = geo . (geo . g - K^T gf)   (gf may be NULL)
+ *   restrict_adj:     gx = d fc / d x   applied to g  (g [B, 1, Hc, Wc] -> gx [B, C, H, W])
+ *   prolong_adj:      ge = d out / d e  applied to g  (g [B, 1, H, W]  -> ge [B, C, Hc, Wc])
+ *   transfer_weight_grad: gw[ch][k] = scale * sum_{(a, b)} cf[ch_c][a][b] * ff[ch_f][2a-1+ky][2b-1+kx],
+ *     (a, b) over the coarse interior (interior = 1, restriction) or all coarse nodes (0,
+ *     prolongation); ch_c = ch when c_split else 0, ch_f likewise; gw is [C, 9]; ws holds
+ *     fea_transfer_weight_grad_ws_bytes(C, B, Hc, Wc) bytes; fixed-order (deterministic) sums.
+ *     Restriction weights: cf = g, ff = x (split).  Prolongation weights: cf = e (split), ff = g. */
+int fea_knet_apply_adj_f32(const float* g, float* out, const uint8_t* pid, const float* ktab, int ntab,
+                           int B, int H, int W, void* stream);
+int fea_knet_apply_adj_f64(const double* g, double* out, const uint8_t* pid, const double* ktab, int ntab,
+                           int B, int H, int W, void* stream);
+int fea_jacobi_sweep_adj_f32(const float* g, float* gu, float* gf, const uint8_t* pid, const float* ktab,
+                             const float* omd, int ntab, const float* geo, long long geo_bs, int B, int H,
+                             int W, void* stream);
+int fea_jacobi_sweep_adj_f64(const double* g, double* gu, double* gf, const uint8_t* pid,
+                             const double* ktab, const double* omd, int ntab, const double* geo,
+                             long long geo_bs, int B, int H, int W, void* stream);
+int fea_restrict_adj_f32(const float* g, int C, float* gx, const uint8_t* pid, const float* rtab, int ntab,
+                         float w0, int B, int H, int W, void* stream);
+int fea_restrict_adj_f64(const double* g, int C, double* gx, const uint8_t* pid, const double* rtab,
+                         int ntab, double w0, int B, int H, int W, void* stream);
+int fea_prolong_adj_f32(const float* g, int C, float* ge, const uint8_t* pidc, const float* ptab, int ntab,
+                        float w1, int B, int Hc, int Wc, void* stream);
+int fea_prolong_adj_f64(const double* g, int C, double* ge, const uint8_t* pidc, const double* ptab,
+                        int ntab, double w1, int B, int Hc, int Wc, void* stream);
+int fea_transfer_weight_grad_f32(const float* cf, int c_split, const float* ff, int f_split, int C,
+                                 int interior, float scale, float* gw, double* ws, int B, int Hc, int Wc,
+                                 void* stream);
+int fea_transfer_weight_grad_f64(const double* cf, int c_split, const double* ff, int f_split, int C,
+                                 int interior, double scale, double* gw, double* ws, int B, int Hc, int Wc,
+                                 void* stream);
+size_t fea_transfer_weight_grad_ws_bytes_f32(int C, int B, int Hc, int Wc);
+size_t fea_transfer_weight_grad_ws_bytes_f64(int C, int B, int Hc, int Wc);
+
 /* ---------------------------------------------------------------------------
  * (2) Framed multigrid-level ops (MultigridSolver), H x W grids (H, W >= 3; the intergrid ops need
  *     odd H and W: the coarse grid is (H+1)/2 x (W+1)/2, fine nodes (2I, 2J) on coarse (I, J)).

@@ -247,6 +247,199 @@ __global__ __launch_bounds__(256) void k_norm_partial(const T* __restrict__ u, c
   }
 }
 
+// ---------------------------------------------------------------------------
+// Adjoints for autograd (MultiGrid.forward / qm training, FEANet/multigrid.py:132-157)
+// ---------------------------------------------------------------------------
+// K^T g: y = K u has y[i] = sum_d W_{p(i+d)}[d] u[i+d], so (K^T g)[j] = sum_d W_{p(j)}[d] g[j-d].
+template <typename T>
+__global__ __launch_bounds__(256) void k_knet_adj(const T* __restrict__ g, T* __restrict__ out,
+                                                  const uint8_t* __restrict__ pid, const T* __restrict__ ktab,
+                                                  int ntab, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, ktab, ntab * 9);
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W;
+  const T* gb = g + blockIdx.z * HW;
+  const int p = pid ? pid[(long long)r * W + c] : 0;
+  T acc = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const int rr = r - (dr - 1);
+    if (rr < 0 || rr >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int cc = c - (dc - 1);
+      if (cc < 0 || cc >= W) continue;
+      acc += tab[p * 9 + dr * 3 + dc] * gb[(long long)rr * W + cc];
+    }
+  }
+  out[blockIdx.z * HW + (long long)r * W + c] = acc;
+}
+
+// Jacobi-sweep adjoint (k_jacobi above; bc carries no gradient).  With g' = geo . g:
+//   grad_f = omd . g'          grad_u = geo . (g' - K^T grad_f)
+template <typename T>
+__global__ __launch_bounds__(256) void k_jacobi_adj(const T* __restrict__ g, T* __restrict__ gu, T* __restrict__ gf,
+                                                    const uint8_t* __restrict__ pid, const T* __restrict__ ktab,
+                                                    const T* __restrict__ omd, int ntab, const T* __restrict__ geo,
+                                                    long long geo_bs, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 10];
+  for (int i = threadIdx.y * blockDim.x + threadIdx.x; i < ntab * 10; i += blockDim.x * blockDim.y)
+    tab[i] = (i % 10 == 9) ? omd[i / 10] : ktab[(i / 10) * 9 + (i % 10)];
+  __syncthreads();
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= H || c >= W) return;
+  const long long HW = (long long)H * W;
+  const T* gb = g + blockIdx.z * HW;
+  const T* geob = geo ? geo + blockIdx.z * geo_bs : nullptr;
+  auto gm = [&](long long j, int rr, int cc) -> T {
+    return geob ? geob[j] : T((rr > 0 && rr < H - 1 && cc > 0 && cc < W - 1) ? 1 : 0);
+  };
+  const long long i = (long long)r * W + c;
+  const int p = pid ? pid[i] : 0;
+  T acc = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const int rr = r - (dr - 1);
+    if (rr < 0 || rr >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int cc = c - (dc - 1);
+      if (cc < 0 || cc >= W) continue;
+      const long long j = (long long)rr * W + cc;
+      const int q = pid ? pid[j] : 0;
+      acc += tab[p * 10 + dr * 3 + dc] * (tab[q * 10 + 9] * (gm(j, rr, cc) * gb[j]));
+    }
+  }
+  const T gi = gm(i, r, c);
+  const T g1 = gi * gb[i];
+  gu[blockIdx.z * HW + i] = gi * (g1 - acc);
+  if (gf) gf[blockIdx.z * HW + i] = tab[p * 10 + 9] * g1;
+}
+
+// Restriction adjoint w.r.t. its (split, C-channel) input: gx[ch][y][x] = w0 * sum over interior coarse
+// (I, J) whose 3x3 window holds (y, x) of R_ch[y-2I+1][x-2J+1] * g[I][J]  (C == 1: kernel by pid).
+template <typename T>
+__global__ __launch_bounds__(256) void k_restrict_adj(const T* __restrict__ g, int C, T* __restrict__ gx,
+                                                      const uint8_t* __restrict__ pid, const T* __restrict__ rtab,
+                                                      int ntab, T w0, int H, int W) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, rtab, ntab * 9);
+  __syncthreads();
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int x = blockIdx.x * kBX + threadIdx.x, y = blockIdx.y * kBY + threadIdx.y;
+  if (y >= H || x >= W) return;
+  const long long HW = (long long)H * W;
+  const T* gb = g + (long long)blockIdx.z * Hc * Wc;
+  const int p = (C == 1 && pid) ? pid[(long long)y * W + x] : 0;
+  for (int ch = 0; ch < C; ++ch) {
+    const int t = C == 1 ? p : ch;
+    T acc = 0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int ty = y + 1 - ky;  // = 2I
+      if (ty & 1) continue;
+      const int I = ty >> 1;
+      if (I < 1 || I > Hc - 2) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tx = x + 1 - kx;
+        if (tx & 1) continue;
+        const int J = tx >> 1;
+        if (J < 1 || J > Wc - 2) continue;
+        acc += tab[t * 9 + ky * 3 + kx] * gb[(long long)I * Wc + J];
+      }
+    }
+    gx[((long long)blockIdx.z * C + ch) * HW + (long long)y * W + x] = w0 * acc;
+  }
+}
+
+// Prolongation adjoint w.r.t. its (split, C-channel) input: ge[ch][a][b] = w1 * sum_k P_ch[k] *
+// g[2a-1+ky][2b-1+kx] over fine nodes inside the grid  (C == 1: kernel by the coarse pid).
+template <typename T>
+__global__ __launch_bounds__(256) void k_prolong_adj(const T* __restrict__ g, int C, T* __restrict__ ge,
+                                                     const uint8_t* __restrict__ pidc, const T* __restrict__ ptab,
+                                                     int ntab, T w1, int Hc, int Wc) {
+  __shared__ T tab[FEA_MAX_PATTERNS * 9];
+  load_table(tab, ptab, ntab * 9);
+  __syncthreads();
+  const int H = 2 * Hc - 1, W = 2 * Wc - 1;
+  const int b = blockIdx.x * kBX + threadIdx.x, a = blockIdx.y * kBY + threadIdx.y;
+  if (a >= Hc || b >= Wc) return;
+  const long long HWc = (long long)Hc * Wc;
+  const T* gb = g + (long long)blockIdx.z * H * W;
+  const int p = (C == 1 && pidc) ? pidc[(long long)a * Wc + b] : 0;
+  for (int ch = 0; ch < C; ++ch) {
+    const int t = C == 1 ? p : ch;
+    T acc = 0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int y = 2 * a - 1 + ky;
+      if (y < 0 || y >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int x = 2 * b - 1 + kx;
+        if (x < 0 || x >= W) continue;
+        acc += tab[t * 9 + ky * 3 + kx] * gb[(long long)y * W + x];
+      }
+    }
+    ge[((long long)blockIdx.z * C + ch) * HWc + (long long)a * Wc + b] = w1 * acc;
+  }
+}
+
+// Gradient of the 3x3 inter-grid kernels: per block partial sums of
+//   gw[ch][k] = sum_{(a, b)} cf[chc][a][b] * ff[chf][2a-1+ky][2b-1+kx]
+// over coarse (a, b) in [a0, Hc-a0) x [a0, Wc-a0) (a0 = 1: restriction interior, 0: prolongation),
+// fine indices outside the grid contribute 0; chc = ch if c_split else 0, chf likewise.
+template <typename T>
+__global__ __launch_bounds__(256) void k_tapgrad_partial(const T* __restrict__ cf, int c_split,
+                                                         const T* __restrict__ ff, int f_split, int C, int a0,
+                                                         int Hc, int Wc, double* __restrict__ part) {
+  __shared__ double red[kBY][FEA_MAX_PATTERNS * 9];
+  const int H = 2 * Hc - 1, W = 2 * Wc - 1;
+  const int b = blockIdx.x * kBX + threadIdx.x, a = blockIdx.y * kBY + threadIdx.y;
+  const bool in = a >= a0 && a < Hc - a0 && b >= a0 && b < Wc - a0;
+  const long long HWc = (long long)Hc * Wc, HW = (long long)H * W;
+  for (int ch = 0; ch < C; ++ch) {
+    const T* cb = cf + ((long long)blockIdx.z * (c_split ? C : 1) + (c_split ? ch : 0)) * HWc;
+    const T* fb = ff + ((long long)blockIdx.z * (f_split ? C : 1) + (f_split ? ch : 0)) * HW;
+    const double cv = in ? (double)cb[(long long)a * Wc + b] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int y = 2 * a - 1 + k / 3, x = 2 * b - 1 + k % 3;
+      double v = 0.0;
+      if (in && y >= 0 && y < H && x >= 0 && x < W) v = cv * (double)fb[(long long)y * W + x];
+      v = wave_sum(v);
+      if (lane_id() == 0) red[threadIdx.y][ch * 9 + k] = v;
+    }
+  }
+  __syncthreads();
+  const int tid = threadIdx.y * kBX + threadIdx.x;
+  const long long nb = (long long)gridDim.x * gridDim.y * gridDim.z;
+  const long long blk = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  for (int i = tid; i < C * 9; i += kBX * kBY)
+    part[(long long)i * nb + blk] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+}
+
+// Fixed-order sum of the partials of each of the n outputs (one block per output).
+template <typename T>
+__global__ __launch_bounds__(256) void k_tapgrad_final(const double* __restrict__ part, long long nb, T scale,
+                                                       T* __restrict__ out) {
+  __shared__ double sh[256];
+  const double* p = part + blockIdx.x * nb;
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < nb; i += 256) s += p[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = (T)((double)scale * sh[0]);
+}
+
 }  // namespace fea
 
 using namespace fea;
@@ -318,5 +511,61 @@ static inline bool bad_shape(int B, int H, int W) { return B <= 0 || H <= 0 || W
     FEA_LAUNCH_CHECK();                                                                                  \
   }
 
+#define FEA_ADJOINT_API(SUF, T)                                                                          \
+  extern "C" int fea_knet_apply_adj_##SUF(const T* g, T* out, const uint8_t* pid, const T* ktab, int ntab,  \
+                                          int B, int H, int W, void* stream) {                           \
+    if (!g || !out || !ktab || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W) || g == out)     \
+      return FEA_EINVAL;                                                                                 \
+    k_knet_adj<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(g, out, pid, ktab, ntab,  \
+                                                                                  H, W);                 \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_jacobi_sweep_adj_##SUF(const T* g, T* gu, T* gf, const uint8_t* pid, const T* ktab,    \
+                                            const T* omd, int ntab, const T* geo, long long geo_bs, int B,   \
+                                            int H, int W, void* stream) {                                    \
+    if (!g || !gu || !ktab || !omd || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W) || g == gu ||  \
+        g == gf)                                                                                            \
+      return FEA_EINVAL;                                                                                     \
+    k_jacobi_adj<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(g, gu, gf, pid, ktab, omd,  \
+                                                                                    ntab, geo, geo_bs, H, W); \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
+  extern "C" int fea_restrict_adj_##SUF(const T* g, int C, T* gx, const uint8_t* pid, const T* rtab,     \
+                                        int ntab, T w0, int B, int H, int W, void* stream) {             \
+    if (!g || !gx || !rtab || C < 1 || bad_shape(B, H, W) || H < 3 || W < 3 || !(H & 1) || !(W & 1))      \
+      return FEA_EINVAL;                                                                                 \
+    if ((C == 1 && (ntab < 1 || ntab > FEA_MAX_PATTERNS)) || (C > 1 && (ntab != C || C > FEA_MAX_PATTERNS))) \
+      return FEA_EINVAL;                                                                                 \
+    k_restrict_adj<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(g, C, gx, pid, rtab, \
+                                                                                      ntab, w0, H, W);   \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_prolong_adj_##SUF(const T* g, int C, T* ge, const uint8_t* pidc, const T* ptab,     \
+                                       int ntab, T w1, int B, int Hc, int Wc, void* stream) {            \
+    if (!g || !ge || !ptab || C < 1 || bad_shape(B, Hc, Wc) || Hc < 2 || Wc < 2) return FEA_EINVAL;      \
+    if ((C == 1 && (ntab < 1 || ntab > FEA_MAX_PATTERNS)) || (C > 1 && (ntab != C || C > FEA_MAX_PATTERNS))) \
+      return FEA_EINVAL;                                                                                 \
+    k_prolong_adj<T><<<grid_for(Hc, Wc, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(g, C, ge, pidc, ptab, \
+                                                                                      ntab, w1, Hc, Wc); \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_transfer_weight_grad_##SUF(const T* cf, int c_split, const T* ff, int f_split, int C,  \
+                                                int interior, T scale, T* gw, double* ws, int B, int Hc,   \
+                                                int Wc, void* stream) {                                  \
+    if (!cf || !ff || !gw || !ws || C < 1 || C > FEA_MAX_PATTERNS || bad_shape(B, Hc, Wc) || Hc < 2 || Wc < 2) \
+      return FEA_EINVAL;                                                                                 \
+    const dim3 gr = grid_for(Hc, Wc, B);                                                                 \
+    k_tapgrad_partial<T><<<gr, dim3(kBX, kBY), 0, (hipStream_t)stream>>>(cf, c_split, ff, f_split, C,    \
+                                                                          interior ? 1 : 0, Hc, Wc, ws);  \
+    k_tapgrad_final<T><<<C * 9, 256, 0, (hipStream_t)stream>>>(ws, (long long)gr.x * gr.y * gr.z, scale, gw); \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" size_t fea_transfer_weight_grad_ws_bytes_##SUF(int C, int B, int Hc, int Wc) {              \
+    const dim3 gr = grid_for(Hc, Wc, B);                                                                 \
+    return (size_t)C * 9 * gr.x * gr.y * gr.z * sizeof(double);                                          \
+  }
+
 FEA_GENERIC_API(f32, float)
 FEA_GENERIC_API(f64, double)
+FEA_ADJOINT_API(f32, float)
+FEA_ADJOINT_API(f64, double)

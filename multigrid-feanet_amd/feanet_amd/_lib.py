@@ -28,6 +28,12 @@ _SIGS = {
     "restrict": [P, I, P, P, P, I, "S", I, I, I, P],
     "prolong": [P, I, P, P, P, P, I, "S", I, I, I, P],
     "residual_norm": [P, P, P, P, I, P, P, I, I, I, P],
+    # adjoints (autograd)
+    "knet_apply_adj": [P, P, P, P, I, I, I, I, P],
+    "jacobi_sweep_adj": [P, P, P, P, P, P, I, P, LL, I, I, I, P],
+    "restrict_adj": [P, I, P, P, P, I, "S", I, I, I, P],
+    "prolong_adj": [P, I, P, P, P, I, "S", I, I, I, P],
+    "transfer_weight_grad": [P, I, P, I, I, I, "S", P, P, I, I, I, P],
     # framed level ops: (..., B, H, W, ld, bstride[, ldc, bstridec], stream)
     "mg_pack": [P, P, P, LL, P, LL, I, I, I, I, LL, P],
     "mg_unpack": [P, P, I, I, I, I, LL, P],
@@ -46,6 +52,8 @@ _EXTRA = {
     "fea_mg_layout": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
     "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
+    "fea_transfer_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
+    "fea_transfer_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
 }
 
 _lib = None
@@ -108,6 +116,10 @@ TAIL_LDS_LIMIT = 160 * 1024 - 1024
 
 def coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, multi):
     return int(lib().fea_mg_coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, int(bool(multi))))
+
+
+def weight_grad_ws_bytes(C, B, Hc, Wc):
+    return int(lib().fea_transfer_weight_grad_ws_bytes_f64(C, B, Hc, Wc))
 
 
 def norm_workspace_bytes(B, H, W):

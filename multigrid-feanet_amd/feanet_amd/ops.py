@@ -65,7 +65,7 @@ def _bhw(x):
     return B, H, W
 
 
-def knet_apply(u, ktab, pid=None):
+def _knet_apply(u, ktab, pid=None):
     """y = K u with per-node-pattern stencils (KNet.forward, FEANet/model.py:22-30)."""
     u = _field(u, "u")
     B, H, W = _bhw(u)
@@ -77,12 +77,9 @@ def knet_apply(u, ktab, pid=None):
     return y
 
 
-def conv3x3(x, w):
-    """Single-channel 3x3 cross-correlation, zero padding (FNet.forward, HNet layers)."""
-    return knet_apply(x, w, None)
 
 
-def split_x(x, pid, C):
+def _split_x(x, pid, C):
     """x_split[:, p] = mask_p * x (KNet.split_x, FEANet/model.py:37-47); x is [B, 1, H, W]."""
     x = _field(x, "x")
     B, H, W = _bhw(x)
@@ -102,7 +99,7 @@ def _bcast_stride(t, B, H, W, name, dtype, device):
     return t, (0 if nb == 1 else H * W)
 
 
-def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
+def _jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
     """One weighted-Jacobi sweep with Dirichlet reset (JacobiBlock.jacobi_convolution,
     FEANet/jacobi.py:39-47).  geo/bc None = square domain / zero boundary values."""
     u = _field(u, "u")
@@ -123,7 +120,7 @@ def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
     return out
 
 
-def residual(u, f, ktab, pid=None):
+def _residual(u, f, ktab, pid=None):
     """r = f - K u."""
     u = _field(u, "u")
     f = _field(f, "f", u.dtype)
@@ -136,7 +133,7 @@ def residual(u, f, ktab, pid=None):
     return r
 
 
-def restrict(x, rtab, w0=1.0, pid=None):
+def _restrict(x, rtab, w0=1.0, pid=None):
     """Restriction (RestrictionNet + MultiGrid.Restrict, FEANet/multigrid.py:50-60,115-122):
     x [B, C, H, W]; C > 1 means x is already split (one kernel per channel); C == 1 uses
     the kernel of each fine node's pattern (pid) or rtab[0]."""
@@ -155,7 +152,7 @@ def restrict(x, rtab, w0=1.0, pid=None):
     return out
 
 
-def prolong(e, ptab, w1=1.0, pidc=None, add=None):
+def _prolong(e, ptab, w1=1.0, pidc=None, add=None):
     """Prolongation (ProlongationNet + MultiGrid.Interpolate, FEANet/multigrid.py:62-73,124-130):
     out = add + w1 * conv_transpose2d(e, P, stride 2, pad 1); e [B, C, Hc, Wc]."""
     e = _field(e, "e")
@@ -192,3 +189,71 @@ def residual_norm(u, f=None, ktab=None, pid=None):
     _lib.call("residual_norm", u.dtype, u.data_ptr(), _ptr(f), _ptr(pid) if f is not None else None,
               _ptr(tab), 0 if tab is None else tab.shape[0], out.data_ptr(), ws.data_ptr(), B, H, W, _stream(u))
     return out
+
+
+# ---------------------------------------------------------------------------- public entry points
+# Each op runs its HIP kernel directly, or through the torch.autograd.Function of autograd.py
+# (HIP forward + HIP adjoint) when autograd has to record it.  Stencil / omega-over-d / geometry
+# tables are constants of the operator (the reference freezes them, multigrid.py:45-47): a table
+# that merely carries requires_grad (nn.Conv2d default) does not by itself start a graph.
+
+def _grad(*ts):
+    return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+
+
+def knet_apply(u, ktab, pid=None):
+    """y = K u with per-node-pattern stencils (KNet.forward, FEANet/model.py:22-30)."""
+    if _grad(u):
+        from . import autograd
+        return autograd.KNetApply.apply(u, ktab, pid)
+    return _knet_apply(u, ktab, pid)
+
+
+def conv3x3(x, w):
+    """Single-channel 3x3 cross-correlation, zero padding (FNet.forward, HNet layers)."""
+    return knet_apply(x, w, None)
+
+
+def split_x(x, pid, C):
+    """x_split[:, p] = mask_p * x (KNet.split_x, FEANet/model.py:37-47); x is [B, 1, H, W]."""
+    if _grad(x):
+        from . import autograd
+        return autograd.SplitX.apply(x, pid, C)
+    return _split_x(x, pid, C)
+
+
+def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
+    """One weighted-Jacobi sweep with Dirichlet reset (JacobiBlock.jacobi_convolution,
+    FEANet/jacobi.py:39-47).  geo/bc None = square domain / zero boundary values."""
+    if _grad(u, f):
+        from . import autograd
+        return autograd.JacobiSweep.apply(u, f, ktab, omd, pid, geo, bc)
+    return _jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
+
+
+def residual(u, f, ktab, pid=None):
+    """r = f - K u."""
+    if _grad(u, f):
+        from . import autograd
+        return autograd.Residual.apply(u, f, ktab, pid)
+    return _residual(u, f, ktab, pid)
+
+
+def restrict(x, rtab, w0=1.0, pid=None):
+    """Restriction (RestrictionNet + MultiGrid.Restrict, FEANet/multigrid.py:50-60,115-122):
+    x [B, C, H, W]; C > 1 means x is already split (one kernel per channel); C == 1 uses
+    the kernel of each fine node's pattern (pid) or rtab[0].  Differentiable in x and rtab."""
+    if _grad(x, rtab):
+        from . import autograd
+        return autograd.Restrict.apply(x, rtab, w0, pid)
+    return _restrict(x, rtab, w0, pid)
+
+
+def prolong(e, ptab, w1=1.0, pidc=None, add=None):
+    """Prolongation (ProlongationNet + MultiGrid.Interpolate, FEANet/multigrid.py:62-73,124-130):
+    out = add + w1 * conv_transpose2d(e, P, stride 2, pad 1); e [B, C, Hc, Wc].
+    Differentiable in e, ptab and add."""
+    if _grad(e, ptab, add):
+        from . import autograd
+        return autograd.Prolong.apply(e, ptab, w1, pidc, add)
+    return _prolong(e, ptab, w1, pidc, add)

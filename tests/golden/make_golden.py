@@ -456,6 +456,38 @@ def multigrid_py_runs():
     save("multigrid_py_iface65.npz", **out)
 
 
+def multigrid_py_training():
+    """FEANet/multigrid.py training forward (MultiGrid.forward + qm, :132-157) and its backward:
+    the gradients of q_m w.r.t. the 16-channel restriction / prolongation kernels (§8f row 2).
+    np.random is seeded right before forward(), which draws the random initial guesses."""
+    lin = torch.asarray([[1, 2, 1], [2, 4, 2], [1, 2, 1]], dtype=torch.float32)
+    sd = torch.load(os.path.join(REF, "Model/learn_intergrid_operator/multigrid_rhs_qm/"
+                                      "model_multigrid_interface_ratio.pth"), weights_only=True)
+    out = {}
+    for n, B, tag in ((16, 2, "linear"), (32, 2, "learned")):
+        mg = ref_mg.MultiGrid(n, lin / 16.0, lin / 4.0, torch.tensor([4.0, 1.0]))
+        if tag == "learned":
+            mg.load_state_dict(sd)
+        seed(100 + n)
+        F1 = torch.from_numpy(np.random.default_rng(n).random((B, 1, n + 1, n + 1)).astype(np.float32))
+        np.random.seed(1000 + n)
+        u = mg(F1)
+        loss = mg.qm(u)
+        loss.backward()
+        k = f"n{n}_"
+        out[k + "F"] = t2n(F1)
+        out[k + "v0"] = t2n(mg.v)
+        out[k + "u"] = t2n(u)
+        out[k + "loss"] = np.array(loss.item())
+        out[k + "rtab"] = t2n(mg.conv.net.weight)[0]
+        out[k + "ptab"] = t2n(mg.deconv.net.weight)[:, 0]
+        out[k + "w"] = t2n(mg.w)
+        out[k + "grad_R"] = t2n(mg.conv.net.weight.grad)[0]
+        out[k + "grad_P"] = t2n(mg.deconv.net.weight.grad)[:, 0]
+        print(f"multigrid.py training n={n}: q_m={loss.item():.6f}")
+    save("multigrid_py_training.npz", **out)
+
+
 def recorded_outputs():
     """Known answers the reference's notebooks hold in their stored outputs."""
     import re
@@ -509,6 +541,7 @@ if __name__ == "__main__":
     mm_convergence_runs()
     mm_interface_run()
     multigrid_py_runs()
+    multigrid_py_training()
     dataset_fixtures()
     recorded_outputs()
     weights()
