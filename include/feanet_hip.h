@@ -160,6 +160,16 @@ int fea_transfer_weight_grad_f32(const float* cf, int c_split, const float* ff, 
 int fea_transfer_weight_grad_f64(const double* cf, int c_split, const double* ff, int f_split, int C,
                                  int interior, double scale, double* gw, double* ws, int B, int Hc, int Wc,
                                  void* stream);
+/* Stencil-weight gradient of y = K u (and of conv3x3: ntab = 1, pid = NULL):
+ *   gw[p][d] = scale * sum_i g[i] u[i+d] [pid(i+d) == p],  gw [ntab, 9]; ws holds
+ *   fea_stencil_weight_grad_ws_bytes(ntab, B, H, W) bytes; fixed-order sums.  KNet / FNet / HNet
+ *   weights (FEANet/model.py:22-30, 49-61; HNet M-FEANet-mg_test.ipynb:97-106). */
+int fea_stencil_weight_grad_f32(const float* g, const float* u, const uint8_t* pid, int ntab, float scale,
+                                float* gw, double* ws, int B, int H, int W, void* stream);
+int fea_stencil_weight_grad_f64(const double* g, const double* u, const uint8_t* pid, int ntab, double scale,
+                                double* gw, double* ws, int B, int H, int W, void* stream);
+size_t fea_stencil_weight_grad_ws_bytes_f32(int ntab, int B, int H, int W);
+size_t fea_stencil_weight_grad_ws_bytes_f64(int ntab, int B, int H, int W);
 size_t fea_transfer_weight_grad_ws_bytes_f32(int C, int B, int Hc, int Wc);
 size_t fea_transfer_weight_grad_ws_bytes_f64(int C, int B, int Hc, int Wc);
 

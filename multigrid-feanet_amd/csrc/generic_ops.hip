@@ -423,6 +423,40 @@ __global__ __launch_bounds__(256) void k_tapgrad_partial(const T* __restrict__ c
     part[(long long)i * nb + blk] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
 }
 
+// Gradient of the per-pattern stencils of y = K u (k_knet): per block partial sums of
+//   gw[p][d] = sum_i g[i] * u[i+d] * [pid(i+d) == p]      (zero padding; pid == NULL: p = 0)
+// Also the weight gradient of conv3x3 (FNet, HNet layers): ntab = 1, no pid.
+template <typename T>
+__global__ __launch_bounds__(256) void k_stencil_wgrad_partial(const T* __restrict__ g, const T* __restrict__ u,
+                                                               const uint8_t* __restrict__ pid, int ntab, int H,
+                                                               int W, double* __restrict__ part) {
+  __shared__ double red[kBY][FEA_MAX_PATTERNS * 9];
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  const bool in = r < H && c < W;
+  const long long HW = (long long)H * W;
+  const T* gb = g + blockIdx.z * HW;
+  const T* ub = u + blockIdx.z * HW;
+  const double gi = in ? (double)gb[(long long)r * W + c] : 0.0;
+#pragma unroll
+  for (int d = 0; d < 9; ++d) {
+    const int rr = r + d / 3 - 1, cc = c + d % 3 - 1;
+    const bool ok = in && rr >= 0 && rr < H && cc >= 0 && cc < W;
+    const long long j = (long long)rr * W + cc;
+    const double v = ok ? gi * (double)ub[j] : 0.0;
+    const int pj = (ok && pid) ? pid[j] : 0;
+    for (int p = 0; p < ntab; ++p) {
+      const double s = wave_sum(pj == p ? v : 0.0);
+      if (lane_id() == 0) red[threadIdx.y][p * 9 + d] = s;
+    }
+  }
+  __syncthreads();
+  const int tid = threadIdx.y * kBX + threadIdx.x;
+  const long long nb = (long long)gridDim.x * gridDim.y * gridDim.z;
+  const long long blk = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  for (int i = tid; i < ntab * 9; i += kBX * kBY)
+    part[(long long)i * nb + blk] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+}
+
 // Fixed-order sum of the partials of each of the n outputs (one block per output).
 template <typename T>
 __global__ __launch_bounds__(256) void k_tapgrad_final(const double* __restrict__ part, long long nb, T scale,
@@ -559,6 +593,18 @@ static inline bool bad_shape(int B, int H, int W) { return B <= 0 || H <= 0 || W
                                                                           interior ? 1 : 0, Hc, Wc, ws);  \
     k_tapgrad_final<T><<<C * 9, 256, 0, (hipStream_t)stream>>>(ws, (long long)gr.x * gr.y * gr.z, scale, gw); \
     FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_stencil_weight_grad_##SUF(const T* g, const T* u, const uint8_t* pid, int ntab, T scale, \
+                                               T* gw, double* ws, int B, int H, int W, void* stream) {      \
+    if (!g || !u || !gw || !ws || ntab < 1 || ntab > FEA_MAX_PATTERNS || bad_shape(B, H, W)) return FEA_EINVAL; \
+    const dim3 gr = grid_for(H, W, B);                                                                   \
+    k_stencil_wgrad_partial<T><<<gr, dim3(kBX, kBY), 0, (hipStream_t)stream>>>(g, u, pid, ntab, H, W, ws); \
+    k_tapgrad_final<T><<<ntab * 9, 256, 0, (hipStream_t)stream>>>(ws, (long long)gr.x * gr.y * gr.z, scale, gw); \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" size_t fea_stencil_weight_grad_ws_bytes_##SUF(int ntab, int B, int H, int W) {              \
+    const dim3 gr = grid_for(H, W, B);                                                                   \
+    return (size_t)ntab * 9 * gr.x * gr.y * gr.z * sizeof(double);                                       \
   }                                                                                                      \
   extern "C" size_t fea_transfer_weight_grad_ws_bytes_##SUF(int C, int B, int Hc, int Wc) {              \
     const dim3 gr = grid_for(Hc, Wc, B);                                                                 \

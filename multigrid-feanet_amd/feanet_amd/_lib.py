@@ -34,6 +34,7 @@ _SIGS = {
     "restrict_adj": [P, I, P, P, P, I, "S", I, I, I, P],
     "prolong_adj": [P, I, P, P, P, I, "S", I, I, I, P],
     "transfer_weight_grad": [P, I, P, I, I, I, "S", P, P, I, I, I, P],
+    "stencil_weight_grad": [P, P, P, I, "S", P, P, I, I, I, P],
     # framed level ops: (..., B, H, W, ld, bstride[, ldc, bstridec], stream)
     "mg_pack": [P, P, P, LL, P, LL, I, I, I, I, LL, P],
     "mg_unpack": [P, P, I, I, I, I, LL, P],
@@ -52,6 +53,8 @@ _EXTRA = {
     "fea_mg_layout": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
     "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
+    "fea_stencil_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
+    "fea_stencil_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
     "fea_transfer_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
     "fea_transfer_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
 }
@@ -120,6 +123,10 @@ def coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, multi):
 
 def weight_grad_ws_bytes(C, B, Hc, Wc):
     return int(lib().fea_transfer_weight_grad_ws_bytes_f64(C, B, Hc, Wc))
+
+
+def stencil_grad_ws_bytes(ntab, B, H, W):
+    return int(lib().fea_stencil_weight_grad_ws_bytes_f64(ntab, B, H, W))
 
 
 def norm_workspace_bytes(B, H, W):

@@ -8,10 +8,10 @@ supplies its gradients.  Here every forward op and every adjoint is a HIP kernel
 training step through `FEANet.multigrid.MultiGrid` never leaves the device and never touches a
 CPU fallback.  `feanet_amd.ops` routes to these Functions whenever autograd needs a graph.
 
-Gradients provided (the ones the reference's training path needs, plus the field inputs):
-  knet_apply    d/du                       (KNet weights are frozen, multigrid.py:45-47)
-  jacobi_sweep  d/du, d/df                 (stencil, omega/d, geometry and boundary are buffers)
-  residual      d/du, d/df
+Gradients provided:
+  knet_apply    d/du, d/d(stencils)        (KNet net2 weights; conv3x3 = FNet / HNet layers)
+  jacobi_sweep  d/du, d/df, d/d(stencils)  (omega/d, geometry and boundary values are constants)
+  residual      d/du, d/df, d/d(stencils)
   split_x       d/dx
   restrict      d/dx, d/d(kernels)         (RestrictionNet.net.weight, multigrid.py:50-60)
   prolong       d/de, d/d(kernels), d/dadd (ProlongationNet.net.weight, multigrid.py:62-73)
@@ -24,11 +24,9 @@ from . import _lib, ops
 
 
 def _frozen(ctx, name, *idx):
-    """Raised at backward time only: a forward under grad mode with trainable-looking stencil weights
-    (nn.Conv2d parameters default to requires_grad=True) must keep working as in the reference."""
     if any(ctx.needs_input_grad[i] for i in idx):
-        raise NotImplementedError(f"feanet_amd: no gradient w.r.t. the {name} (the reference's training path "
-                                  "keeps it frozen, multigrid.py:45-47); set requires_grad=False on it")
+        raise NotImplementedError(f"feanet_amd: no gradient w.r.t. the {name} (constants of the operator, "
+                                  "FEANet/jacobi.py:17-37); set requires_grad=False on it")
 
 
 def _like(g, ref):
@@ -45,53 +43,86 @@ def _knet_adj(g, ktab, pid):
     return out
 
 
+def _stencil_grad(g, u, ktab, pid, scale=1.0):
+    """d/dW of sum(g . K u) in ktab's shape/dtype (fea_stencil_weight_grad)."""
+    g, u = g.contiguous(), u.contiguous()
+    B, H, W = ops._bhw(g)
+    ntab = ktab.numel() // 9
+    gw = torch.empty((ntab, 9), dtype=g.dtype, device=g.device)
+    ws = torch.empty(max(1, _lib.stencil_grad_ws_bytes(ntab, B, H, W) // 8), dtype=torch.float64, device=g.device)
+    _lib.call("stencil_weight_grad", g.dtype, g.data_ptr(), u.data_ptr(), ops._ptr(pid if ntab > 1 else None), ntab,
+              float(scale), gw.data_ptr(), ws.data_ptr(), B, H, W, ops._stream(g))
+    return gw.reshape(ktab.shape).to(ktab.dtype)
+
+
 class KNetApply(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u, ktab, pid):
-        ctx.save_for_backward(ktab, pid)
+        ctx.save_for_backward(u if ctx.needs_input_grad[1] else None, ktab, pid)
         return ops._knet_apply(u, ktab, pid)
 
     @staticmethod
     def backward(ctx, g):
-        _frozen(ctx, "stencil table", 1)
-        ktab, pid = ctx.saved_tensors
-        return _knet_adj(g, ktab, pid), None, None
+        u, ktab, pid = ctx.saved_tensors
+        gu = _knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
+        gk = _stencil_grad(g, u, ktab, pid) if ctx.needs_input_grad[1] else None
+        return gu, gk, None
 
 
 class Residual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u, f, ktab, pid):
-        ctx.save_for_backward(ktab, pid)
+        ctx.save_for_backward(u if ctx.needs_input_grad[2] else None, ktab, pid)
         return ops._residual(u, f, ktab, pid)
 
     @staticmethod
     def backward(ctx, g):
-        _frozen(ctx, "stencil table", 2)
-        ktab, pid = ctx.saved_tensors
+        u, ktab, pid = ctx.saved_tensors
         gu = -_knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
-        return gu, (g if ctx.needs_input_grad[1] else None), None, None
+        gk = _stencil_grad(g, u, ktab, pid, -1.0) if ctx.needs_input_grad[2] else None
+        return gu, (g if ctx.needs_input_grad[1] else None), gk, None
 
 
 class JacobiSweep(torch.autograd.Function):
+    """out = R(u0 + omd (f - K u0)), u0 = R(u), R(v) = geo v + bc.  Gradients in u, f and the stencils
+    (omega/d, geometry and boundary values are constants of the block, jacobi.py:17-37)."""
+
     @staticmethod
     def forward(ctx, u, f, ktab, omd, pid, geo, bc):
-        ctx.save_for_backward(ktab, omd, pid, geo)
+        ctx.save_for_backward(u if ctx.needs_input_grad[2] else None, ktab, omd, pid, geo, bc)
         return ops._jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
 
     @staticmethod
     def backward(ctx, g):
-        _frozen(ctx, "stencil / omega-over-d / geometry / boundary values", 2, 3, 5, 6)
-        ktab, omd, pid, geo = ctx.saved_tensors
+        _frozen(ctx, "omega-over-d / geometry / boundary values", 3, 5, 6)
+        u, ktab, omd, pid, geo, bc = ctx.saved_tensors
         g = g.contiguous()
         B, H, W = ops._bhw(g)
         tab = ops._table(ktab, g.dtype, g.device)
         om = torch.as_tensor(omd).to(device=g.device, dtype=g.dtype).reshape(-1).contiguous()
-        geo, gs = ops._bcast_stride(geo, B, H, W, "geometry_idx", g.dtype, g.device)
+        geo_t, gs = ops._bcast_stride(geo, B, H, W, "geometry_idx", g.dtype, g.device)
         gu = torch.empty_like(g)
-        gf = torch.empty_like(g) if ctx.needs_input_grad[1] else None
+        need_gf = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        gf = torch.empty_like(g) if need_gf else None
         _lib.call("jacobi_sweep_adj", g.dtype, g.data_ptr(), gu.data_ptr(), ops._ptr(gf), ops._ptr(pid),
-                  tab.data_ptr(), om.data_ptr(), tab.shape[0], ops._ptr(geo), gs, B, H, W, ops._stream(g))
-        return gu, gf, None, None, None, None, None
+                  tab.data_ptr(), om.data_ptr(), tab.shape[0], ops._ptr(geo_t), gs, B, H, W, ops._stream(g))
+        gk = None
+        if ctx.needs_input_grad[2]:  # d/dW of -sum(gf . K u0)
+            if geo is None:
+                u0 = u * _interior_mask(H, W, u)
+            else:
+                u0 = u * geo
+            if bc is not None:
+                u0 = u0 + bc
+            gk = _stencil_grad(gf, u0.to(g.dtype).expand(g.shape), ktab, pid, -1.0)
+        return (gu if ctx.needs_input_grad[0] else None), (gf if ctx.needs_input_grad[1] else None), gk, \
+            None, None, None, None
+
+
+def _interior_mask(H, W, like):
+    m = torch.zeros((H, W), dtype=like.dtype, device=like.device)
+    m[1:-1, 1:-1] = 1
+    return m
 
 
 class SplitX(torch.autograd.Function):

@@ -193,9 +193,8 @@ def residual_norm(u, f=None, ktab=None, pid=None):
 
 # ---------------------------------------------------------------------------- public entry points
 # Each op runs its HIP kernel directly, or through the torch.autograd.Function of autograd.py
-# (HIP forward + HIP adjoint) when autograd has to record it.  Stencil / omega-over-d / geometry
-# tables are constants of the operator (the reference freezes them, multigrid.py:45-47): a table
-# that merely carries requires_grad (nn.Conv2d default) does not by itself start a graph.
+# (HIP forward + HIP adjoint) when autograd has to record it: as with the reference's conv2d
+# modules, any input (field or weight table) that requires grad starts a graph.
 
 def _grad(*ts):
     return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
@@ -203,7 +202,7 @@ def _grad(*ts):
 
 def knet_apply(u, ktab, pid=None):
     """y = K u with per-node-pattern stencils (KNet.forward, FEANet/model.py:22-30)."""
-    if _grad(u):
+    if _grad(u, ktab):
         from . import autograd
         return autograd.KNetApply.apply(u, ktab, pid)
     return _knet_apply(u, ktab, pid)
@@ -225,7 +224,7 @@ def split_x(x, pid, C):
 def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
     """One weighted-Jacobi sweep with Dirichlet reset (JacobiBlock.jacobi_convolution,
     FEANet/jacobi.py:39-47).  geo/bc None = square domain / zero boundary values."""
-    if _grad(u, f):
+    if _grad(u, f, ktab, omd, geo, bc):
         from . import autograd
         return autograd.JacobiSweep.apply(u, f, ktab, omd, pid, geo, bc)
     return _jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
@@ -233,7 +232,7 @@ def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
 
 def residual(u, f, ktab, pid=None):
     """r = f - K u."""
-    if _grad(u, f):
+    if _grad(u, f, ktab):
         from . import autograd
         return autograd.Residual.apply(u, f, ktab, pid)
     return _residual(u, f, ktab, pid)
