@@ -15,11 +15,16 @@ doubling keeping gr0_l = 2 gr0_{l+1} so the unmodified level kernels pair fine a
 exactly as on one grid.  The level kernels compute every local interior row; ghost rows near the
 slab edge are refreshed by exchanges, deeper ones are redundant work (G_0 rows per side, a few %).
 
-Exchanges per V-cycle (depth = rows refreshed, 3 covers every kernel's reach):
-  after a sweep / prolongation-sweep on level l:   the new iterate of level l
-  after a residual-restriction on level l < Ld-1:  f_{l+1}
+Communication (communication-avoiding).  Every level kernel already computes the ghost rows it
+stores, so ghost rows stay correct to a depth that shrinks by one row per sweep and halves per
+restriction; an exchange is needed only where that depth would run out.  Per V-cycle:
+  after the finest pre-smoothing (or the cycle join):  D1 rows of f_1 (and D0 rows of the
+                                                       pre-smoothed finest iterate, joined cycles)
   at level Ld:  all-gather of the owned rows of f_Ld -> the replicated coarse solve -> local copy
-i.e. 2*Ld - 1 neighbour exchanges (two 3-row messages per neighbour) and one all-gather.
+  after the finest post-smoothing (unjoined cycles):   D0 rows of the finest iterate
+i.e. ONE batch of neighbour messages and one all-gather per V-cycle, whatever Ld.  D0 and D1 are the
+smallest depths for which a row-validity simulation of the schedule (exchange_depths) keeps every
+owned row exact; the result stays bitwise the single-GPU V-cycle.
 """
 import torch
 
@@ -27,8 +32,6 @@ from . import _lib
 from .schedule import vcycle_schedule
 from .solver import MultigridSolver
 
-DEPTH = 3   # rows per halo exchange (f and corrections)
-DEPTH0 = 4  # rows per exchange of the finest iterate (the cycle join reaches 4 rows: x -> v -> w -> r)
 
 
 def global_levels(m, n):
@@ -90,28 +93,184 @@ class Partition:
         return LevelPart(H, s, e, gr0, gend)
 
 
-def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a"):
-    """The distributed part of one V-cycle (levels 0..Ld-1) with its communication steps:
-    kernel steps of feanet_amd.schedule plus ("exchange", l, buf, depth), ("gather",), ("coarse",),
-    ("scatter", dst)."""
+def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a", depths=(4, 4)):
+    """The distributed part of one (unjoined) V-cycle: kernel steps of feanet_amd.schedule plus
+    ("exchange", l, buf, depth), ("gather",), ("coarse",), ("scatter", dst).  depths = (D0, D1)."""
+    D0, D1 = depths
     steps, end = vcycle_schedule(Ld + 1, nu1, nu2, None, start, tail_from=Ld, fuse=fuse)
     out = []
-    for st in steps:
+    for i, st in enumerate(steps):
         kind, l = st[0], st[1]
         if kind == "coarse_tail":
             out += [("gather",), ("coarse",), ("scatter", st[2])]
             continue
         out.append(st)
-        d = DEPTH0 if l == 0 else DEPTH
-        if kind == "sweep":
-            out.append(("exchange", l, st[3], d))
-        elif kind in ("prolong_sweep", "prolong_add"):
-            out.append(("exchange", l, st[4], d))
-        elif kind == "sweep_restrict":
-            out.append(("exchange", l, st[3], d))  # the pre-smoothed iterate: read by a later cycle join
-        if kind in ("resid_restrict", "sweep_restrict") and l + 1 < Ld:
-            out.append(("exchange", l + 1, "f", DEPTH))
+        if kind in ("resid_restrict", "sweep_restrict") and l == 0 and Ld >= 2:
+            out.append(("exchange", 1, "f", D1))
+    out.append(("exchange", 0, end, D0))
     return out, end
+
+
+def _restricted(r):
+    """Ghost depth of a restriction whose fine input is valid to depth r (fine rows 2I-1..2I+1)."""
+    return (r - 1) // 2 if r >= 1 else -1
+
+
+def simulate_validity(program, Ld, ghost, init=None):
+    """Row validity along a list of dd steps: for every (level, buffer) the number of ghost rows past
+    the owned rows that hold the single-grid values (owned rows exact iff >= 0).  Buffers start as in
+    `init` (default: fully valid, as after load()); f_0 is static (fully valid).  Returns False as soon
+    as a kernel would write a wrong owned row, else the final validity map.  Steps may also be
+    ("join", pre, ec_name)."""
+    INF = 1 << 30
+    v = dict(init or {})
+    g = [ghost(l) for l in range(Ld + 1)]
+
+    def get(l, name):
+        if name is None or name == "zero":
+            return INF
+        if name == "f" and l == 0:
+            return g[0]
+        return v.get((l, name), g[l])
+
+    def put(l, name, val):
+        val = min(val, g[l])
+        v[(l, name)] = val
+        return val >= 0
+
+    for st in program:
+        k = st[0]
+        if k == "exchange":
+            l, name, d = st[1], st[2], st[3]
+            if get(l, name) < 0 or d > g[l]:
+                return False
+            v[(l, name)] = max(get(l, name), d)
+        elif k in ("gather", "coarse"):
+            if k == "gather" and get(Ld, "f") < 0:
+                return False
+        elif k == "scatter":
+            v[(Ld, st[1])] = g[Ld]
+        elif k == "sweep":
+            l = st[1]
+            if not put(l, st[3], min(get(l, st[2]) - 1, get(l, "f"))):
+                return False
+        elif k in ("resid_restrict", "sweep_restrict"):
+            l, src, dst = st[1], st[2], st[3]
+            if k == "sweep_restrict" or src is None:
+                it = min(get(l, src) - 1 if src is not None else INF, get(l, "f"))
+                if not put(l, dst, it):
+                    return False
+            else:
+                it = get(l, src)
+            if not put(l + 1, "f", _restricted(min(it - 1, get(l, "f")))):
+                return False
+        elif k in ("prolong_sweep", "prolong_add"):
+            l, src, ec, dst = st[1:5]
+            x = min(get(l, src), 2 * get(l + 1, ec) - 1)
+            if not put(l, dst, (min(x - 1, get(l, "f")) if k == "prolong_sweep" else x)):
+                return False
+        elif k == "join":
+            pre, ec = st[1], st[2]
+            other = "b" if pre == "a" else "a"
+            x = min(get(0, pre), 2 * get(1, ec) - 1)
+            post = min(x - 1, get(0, "f"))
+            nxt = min(post - 1, get(0, "f"))
+            if post < 0 or not put(0, other, nxt) or not put(1, "f", _restricted(min(nxt - 1, get(0, "f")))):
+                return False
+        else:
+            raise ValueError(f"simulate_validity: unknown step {st!r}")
+    return v
+
+
+def exchange_depths(Ld, ghost, nu1=1, nu2=1, fuse=True, joined=True):
+    """Smallest (D0, D1) (by bytes: D1 rows are half as wide) keeping the owned rows exact in every
+    program DDSolver runs.  Across program boundaries only the finest iterate carries over, and every
+    program ends by exchanging it (D0 rows): so checking each program once from the weakest start
+    state (finest iterates valid to exactly D0) covers any sequence of them (induction)."""
+    def programs(D):
+        out = [dd_schedule(Ld, nu1, nu2, fuse, "a", D)[0]]
+        if joined:
+            for njoin in (0, 1, 2):
+                seq, s = [], "a"
+                for kind in ["head"] + ["join"] * njoin + ["tail"]:
+                    st, s = _joined_chunk_steps(Ld, nu1, nu2, fuse, kind, s, D)
+                    seq += st
+                out.append(seq)
+        return out
+
+    def ok(D0, D1):
+        init = {(0, "a"): D0, (0, "b"): D0}
+        return all(simulate_validity(p, Ld, ghost, init) for p in programs((D0, D1)))
+
+    best = None
+    top1 = ghost(1) if Ld >= 2 else 1
+    for D0 in range(1, min(ghost(0), 32) + 1):
+        if not ok(D0, top1):
+            continue
+        lo, hi = 1, top1
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if ok(D0, mid):
+                hi = mid
+            else:
+                lo = mid + 1
+        cost = 2 * D0 + (lo if Ld >= 2 else 0)
+        if best is None or cost < best[0]:
+            best = (cost, (D0, lo))
+    if best is None:
+        raise ValueError(f"exchange_depths: no exchange depths keep the slabs exact (Ld={Ld}); "
+                         "more ghost rows are needed")
+    return best[1]
+
+
+def _joined_chunk_steps(Ld, nu1, nu2, fuse, kind, s, D):
+    """Steps of one chunk of a joined program (see DDSolver.chunk): ("head", start) = SR(0) and its
+    exchanges; ("join", pre) = levels >= 1 of the cycle, then the cycle join; ("tail", pre) = levels
+    >= 1, then the last PS(0).  Returns (steps, state after the chunk) with the cycle join as
+    ("join", pre, ec) (ec = the level-1 correction buffer)."""
+    D0, D1 = D
+    other = lambda x: "b" if x == "a" else "a"
+    s0 = s if kind == "head" else other(s)  # the start buffer of the cycle the chunk belongs to
+    steps, _ = dd_schedule(Ld, nu1, nu2, fuse, s0, D)
+    ps0 = max(i for i, st in enumerate(steps) if st[0] == "prolong_sweep" and st[1] == 0)
+    body = [st for st in steps[1:ps0] if st[0] != "exchange" or st[1] != 0]
+    i_mid = 0
+    while i_mid < len(body) and body[i_mid][0] == "exchange":
+        i_mid += 1
+    if kind == "head":
+        ex = [("exchange", 0, other(s), D0)] + body[:i_mid]
+        return [steps[0]] + ex, other(s)
+    mid = body[i_mid:]
+    if kind == "join":
+        ec = steps[ps0][3]
+        last = [("join", s, ec), ("exchange", 0, other(s), D0)]
+        if Ld >= 2:
+            last.append(("exchange", 1, "f", D1))
+        return mid + last, other(s)
+    ps = steps[ps0]
+    return mid + [ps, ("exchange", 0, ps[4], D0)], other(s)
+
+
+def _joined(nu1, nu2, fuse):
+    """Whether the local solver joins consecutive cycles (MultigridSolver._joinable for a DD slab)."""
+    return nu1 == 1 and nu2 == 1 and fuse
+
+
+def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True):
+    """The slab partition with the fewest ghost rows (G ghost rows at level Ld, doubling per finer
+    level) for which exchange depths exist, and those depths.  Ghost rows are redundant work."""
+    err = None
+    for G in (2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+        try:
+            part = Partition(m, n, P, Ld, G)
+        except ValueError as e:
+            err = e
+            break
+        try:
+            return part, exchange_depths(Ld, part.ghost, nu1, nu2, fuse, joined=_joined(nu1, nu2, fuse))
+        except ValueError as e:
+            err = e
+    raise ValueError(f"DD: no slab partition of {m} rows over {P} ranks with Ld = {Ld}: {err}")
 
 
 def _launch_list(launches, dtype, stream):
@@ -146,7 +305,7 @@ class DDSolver:
         self.Ld = default_agglomeration(rows, n, world, self.L) if agglomerate is None else int(agglomerate)
         if not 1 <= self.Ld <= self.L - 1:
             raise ValueError(f"DDSolver: agglomeration level {self.Ld} outside [1, {self.L - 1}]")
-        self.part = Partition(rows, n, world, self.Ld)
+        self.part, self.depths = _partition_for(rows, n, world, self.Ld, nu1, nu2, fuse)
         self.parts = [self.part.level(l, rank) for l in range(self.Ld + 1)]
         self.dtype, self.B = dtype, batch
         self.device = torch.device(device if device is not None else "cuda")
@@ -161,6 +320,7 @@ class DDSolver:
             Lv = self.local.levels[l]
             assert Lv.H == lp.Hloc and Lv.W == (n >> l) + 1, (l, Lv.H, lp)
         self.coarse_plan, self.coarse_end = self.coarse._build("a")
+        assert self.joinable() == _joined(nu1, nu2, fuse)
         self.use_graph = graph
         self._segs = {}
         self._graphs = {}
@@ -246,7 +406,7 @@ class DDSolver:
             elif st[0] == "coarse":
                 launches = list(self.coarse_plan)
             elif st[0] == "join":
-                launches = [self.local._join_call(st[1], st[2])]
+                launches = [self.local._join_call(st[1], self.local._ptr(1, st[2]))]
             else:
                 launches = [self.local.bind_step(st)]
             if segs and segs[-1][0] == "k":
@@ -266,33 +426,11 @@ class DDSolver:
         if key in self._segs:
             return self._segs[key]
         kind, b = key
-        other = lambda x: "b" if x == "a" else "a"
         if kind == "cycle":
-            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, b)
-            res = (self._segs_of(steps), end)
+            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, b, self.depths)
         else:
-            s0 = b if kind == "head" else other(b)  # the start buffer of the cycle the chunk belongs to
-            steps, _ = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, s0)
-            # [SR(0), exch u0, exch f1] + mid + [PS(0), exch u0]
-            i_mid = 1
-            while steps[i_mid][0] == "exchange":
-                i_mid += 1
-            ps0 = max(i for i, st in enumerate(steps) if st[0] == "prolong_sweep" and st[1] == 0)
-            head, mid = steps[:i_mid], steps[i_mid:ps0]
-            if kind == "head":
-                res = (self._segs_of(head), other(b))
-            else:
-                pre = b
-                ec = self.local.bind_step(steps[ps0])[1][1]
-                if kind == "join":
-                    last = [("join", pre, ec), ("exchange", 0, other(pre), DEPTH0)]
-                    if self.Ld > 1:
-                        last.append(("exchange", 1, "f", DEPTH))
-                else:
-                    _, tail_steps = None, dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, other(pre))[0]
-                    ps = [st for st in tail_steps if st[0] == "prolong_sweep" and st[1] == 0][-1]
-                    last = [ps, ("exchange", 0, ps[4], DEPTH0)]
-                res = (self._segs_of(mid + last), other(pre))
+            steps, end = _joined_chunk_steps(self.Ld, self.nu1, self.nu2, self.fuse, kind, b, self.depths)
+        res = (self._segs_of(steps), end)
         self._segs[key] = res
         return res
 
@@ -419,7 +557,7 @@ class TorchComm:
     def _stage(self, t):
         return t.contiguous() if self.gpu else t.cpu()
 
-    def exchange(self, s, l, name, d=DEPTH):
+    def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])
 
     def exchange_many(self, s, items):
@@ -527,7 +665,7 @@ class LocalGroup:
         for s in self.ranks:
             s._state = end
 
-    def _exchange(self, l, name, d=DEPTH):
+    def _exchange(self, l, name, d):
         for r, s in enumerate(self.ranks):
             lp = s.parts[l]
             if r > 0:

@@ -27,10 +27,11 @@ class OracleRank:
     boundary rows are kept, the framed kernels' semantics)."""
 
     def __init__(self, m, n, P, r, Ld, f, u, nu=(1, 1)):
-        from feanet_amd.dd import Partition, global_levels
+        from feanet_amd.dd import _partition_for, global_levels
         self.m, self.n, self.P, self.r, self.Ld = m, n, P, r, Ld
         self.L = global_levels(m, n)
-        self.part = Partition(m, n, P, Ld)
+        # the partition and exchange depths DDSolver uses (the oracle runs its unjoined cycles)
+        self.part, self.depths = _partition_for(m, n, P, Ld, nu[0], nu[1], fuse=True)
         self.parts = [self.part.level(l, r) for l in range(Ld + 1)]
         self.lv = [orc.Level(n >> l, "poisson", np.float64, m=p.Hloc - 1) for l, p in enumerate(self.parts)]
         B = f.shape[0]
@@ -108,7 +109,7 @@ def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2):
     R = OracleRank(m, n, world, rank, Ld, f, u)
     state = "a"
     for _ in range(cycles):
-        steps, end = dd_schedule(Ld, 1, 1, True, state)
+        steps, end = dd_schedule(Ld, 1, 1, True, state, R.depths)
         for st in steps:
             if st[0] == "exchange":
                 l, name, DEPTH = st[1], st[2], st[3]

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from feanet_amd.dd import DEPTH, DEPTH0, Partition, dd_schedule, default_agglomeration, global_levels
+from feanet_amd.dd import (Partition, _joined_chunk_steps, _partition_for, dd_schedule, default_agglomeration,
+                           exchange_depths, global_levels, simulate_validity)
 from oracle import feanet_oracle as orc
 
 
@@ -29,12 +30,11 @@ def test_partition_invariants(m, n, P, Ld):
                 assert p.gr0 == 2 * q.gr0 and p.Hloc == 2 * q.Hloc - 1  # fine (2I-1, 2I) <-> coarse I locally
                 assert p.s == 2 * q.s - 1  # coarse row I owned with its fine rows (2I-1, 2I)
                 assert p.e == (2 * q.e - 1 if r < P - 1 else H - 1)
-                d = DEPTH0 if l == 0 else DEPTH
+                g = part.ghost(l)
                 if r > 0:
-                    assert p.lo >= d + 1  # exchanged rows + one kept edge row
+                    assert p.lo == g + 1  # ghost rows below the owned rows (+ the kept edge row)
                 if r < P - 1:
-                    assert p.Hloc - p.hi >= d + 1
-                assert p.e - p.s >= DEPTH
+                    assert p.Hloc - p.hi == g
         assert owned == list(range(1, H - 1)), "interior rows owned exactly once"
 
 
@@ -49,12 +49,48 @@ def test_partition_rejects_bad_splits():
 
 
 def test_dd_schedule_comm_counts():
+    """Communication-avoiding schedule: one batch of neighbour messages + one all-gather per cycle."""
     for Ld in (1, 2, 3, 5):
-        steps, end = dd_schedule(Ld)
+        steps, end = dd_schedule(Ld, depths=(4, 9))
         kinds = [s[0] for s in steps]
-        assert kinds.count("exchange") == 2 * Ld - 1 + 1  # + the pre-smoothed iterate (read by a join)
+        assert kinds.count("exchange") == (2 if Ld >= 2 else 1)
         assert kinds.count("gather") == kinds.count("coarse") == kinds.count("scatter") == 1
         assert end in ("a", "b")
+        for kind, s in (("head", "a"), ("join", "b"), ("tail", "b")):
+            st, _ = _joined_chunk_steps(Ld, 1, 1, True, kind, s, (4, 9))
+            ex = [x for x in st if x[0] == "exchange"]
+            assert len(ex) == {"head": 1 + (Ld >= 2), "join": 1 + (Ld >= 2), "tail": 1}[kind]
+
+
+@pytest.mark.parametrize("m,n,P,Ld", [(64, 32, 2, 2), (128, 64, 2, 3), (16384, 8192, 8, 4), (16384, 8192, 8, 6)])
+def test_exchange_depths_minimal(m, n, P, Ld):
+    """The chosen depths keep every program exact; one row less of either does not."""
+    part, (D0, D1) = _partition_for(m, n, P, Ld)
+    init = lambda d: {(0, "a"): d, (0, "b"): d}
+
+    def progs(D):
+        out = [dd_schedule(Ld, 1, 1, True, "a", D)[0]]
+        for nj in (0, 1, 2):
+            seq, s = [], "a"
+            for kind in ["head"] + ["join"] * nj + ["tail"]:
+                st, s = _joined_chunk_steps(Ld, 1, 1, True, kind, s, D)
+                seq += st
+            out.append(seq)
+        return out
+    assert all(simulate_validity(p, Ld, part.ghost, init(D0)) for p in progs((D0, D1)))
+    if D0 > 1:
+        assert not all(simulate_validity(p, Ld, part.ghost, init(D0 - 1)) for p in progs((D0 - 1, D1)))
+    if Ld >= 2 and D1 > 1:
+        assert not all(simulate_validity(p, Ld, part.ghost, init(D0)) for p in progs((D0, D1 - 1)))
+    assert D1 <= part.ghost(1) and D0 <= part.ghost(0)
+
+
+def test_partition_grows_ghosts_when_needed():
+    """V(2,2) at Ld = 4 needs more coarse ghost rows than V(1,1): the partition grows G."""
+    part, _ = _partition_for(4096, 4096, 8, 4, 2, 2)
+    assert part.G > _partition_for(4096, 4096, 8, 4)[0].G
+    with pytest.raises(ValueError):
+        exchange_depths(4, Partition(4096, 4096, 8, 4, 4).ghost, 2, 2, joined=False)
 
 
 def test_default_agglomeration():

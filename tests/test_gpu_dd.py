@@ -24,9 +24,9 @@ def _global_problem(m, n, B, seed=0):
     return f, u0, bc * (1 - inner)
 
 
-def _single(m, n, B, f, u0, bc, cycles):
+def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1)):
     from feanet_amd.solver import MultigridSolver
-    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B)
+    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1])
     s.set_boundary(bc)
     s.set_rhs(f=f)
     s.load(u0)
@@ -37,14 +37,21 @@ def _single(m, n, B, f, u0, bc, cycles):
     return s, out
 
 
-@pytest.mark.parametrize("m,n,P,Ld,B,graph", [(256, 128, 2, 1, 1, True), (512, 256, 4, 2, 2, True),
-                                              (384, 256, 3, 2, 1, False), (1024, 1024, 4, 3, 1, True),
-                                              (2048, 1024, 8, 3, 1, True)])
-def test_dd_local_group_bitwise(m, n, P, Ld, B, graph):
+@pytest.mark.parametrize("m,n,P,Ld,B,graph,nu", [(256, 128, 2, 1, 1, True, (1, 1)), (512, 256, 4, 2, 2, True, (1, 1)),
+                                                 (384, 256, 3, 2, 1, False, (1, 1)),
+                                                 (1024, 1024, 4, 3, 1, True, (1, 1)),
+                                                 (2048, 1024, 8, 3, 1, True, (1, 1)),
+                                                 (2048, 1024, 8, 4, 1, True, (1, 1)),
+                                                 (4096, 512, 4, 5, 1, True, (1, 1)),
+                                                 (1024, 512, 4, 3, 1, True, (2, 2)),
+                                                 (1024, 512, 2, 3, 1, False, (2, 1))])
+def test_dd_local_group_bitwise(m, n, P, Ld, B, graph, nu):
+    """Communication-avoiding exchanges (one neighbour batch per cycle, exchange_depths): every owned
+    row still equals the single-GPU V-cycle bit for bit, also with deeper agglomeration and V(2,2)."""
     from feanet_amd.dd import LocalGroup
     f, u0, bc = _global_problem(m, n, B)
-    s, ref = _single(m, n, B, f, u0, bc, 4)
-    grp = LocalGroup(n, m, P, agglomerate=Ld, batch=B, graph=graph)
+    s, ref = _single(m, n, B, f, u0, bc, 4, nu)
+    grp = LocalGroup(n, m, P, agglomerate=Ld, batch=B, graph=graph, nu1=nu[0], nu2=nu[1])
     assert grp.ranks[0].coarse.tail_from is None or grp.ranks[0].coarse.tail_from + Ld == s.tail_from
     grp.set_rhs(f)
     grp.load(u0, bc)
