@@ -972,6 +972,12 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 // row each.  Per-node arithmetic is exactly that of fea_mg_prolong_sweep then fea_mg_sweep_restrict,
 // so the result is bitwise the unfused sequence.
 // ---------------------------------------------------------------------------
+template <int SECOND, typename X>
+__device__ __forceinline__ X& pick(X& a, X& b) {
+  if constexpr (SECOND) return b;
+  else return a;
+}
+
 template <typename T>
 struct Ovl3 {
   static constexpr int V = Frame<T>::VEC;
@@ -1049,12 +1055,17 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
   for (int q = 0; q < Q; ++q) acc[q] = T(0);
 
   const int ys = 2 * I0 - 4, ye = 2 * I1 + 2;
-  // prefetched inputs of the next step: u(y), f(y-1), pid(y); coarse rows ca = floor(y/2), cbr = ca + 1
-  T nu[V], nf[V];
-  int np[V];
-  vload<T, V>(ub + rowo(ys), nu);
-  vload<T, V>(fb + rowo(ys - 1), nf);
-  if constexpr (MULTI) pload<V>(pb + rowo(ys), np);
+  // inputs u(y), f(y-1), pid(y) in flight two steps ahead, in a ping-pong pair of buffers: even steps
+  // consume and refill A, odd steps B, so no in-flight register is ever copied (a copy would force
+  // the wait for its load at once) — the join runs ~2 waves per SIMD and needs the latency cover
+  T uA[V], fA[V], uB[V], fB[V];
+  int pA[V], pB[V];
+  vload<T, V>(ub + rowo(ys), uA);
+  vload<T, V>(fb + rowo(ys - 1), fA);
+  if constexpr (MULTI) pload<V>(pb + rowo(ys), pA);
+  vload<T, V>(ub + rowo(ys + 1), uB);
+  vload<T, V>(fb + rowo(ys), fB);
+  if constexpr (MULTI) pload<V>(pb + rowo(ys + 1), pB);
   CRow<T, V> Ca = finish_c<T, V, MULTI>(rc(ys / 2));
   CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(ys / 2 + 1));
   RawC<T, V> nC = rc(ys / 2 + 2);
@@ -1074,18 +1085,21 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
 
   auto step = [&](int y, auto par) {
     constexpr int ODD = decltype(par)::value;
-    // this step's inputs, next step's loads
+    // this step's inputs; refill the buffer with the rows two steps ahead
+    T(&bu)[V] = pick<ODD>(uA, uB);
+    T(&bf)[V] = pick<ODD>(fA, fB);
+    int(&bp)[V] = pick<ODD>(pA, pB);
     T u0[V], fy1[V];
     int p0[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      u0[k] = nu[k];
-      fy1[k] = nf[k];
-      if constexpr (MULTI) p0[k] = np[k];
+      u0[k] = bu[k];
+      fy1[k] = bf[k];
+      if constexpr (MULTI) p0[k] = bp[k];
     }
-    vload<T, V>(ub + rowo(y + 1), nu);
-    vload<T, V>(fb + rowo(y), nf);
-    if constexpr (MULTI) pload<V>(pb + rowo(y + 1), np);
+    vload<T, V>(ub + rowo(y + 2), bu);
+    vload<T, V>(fb + rowo(y + 1), bf);
+    if constexpr (MULTI) pload<V>(pb + rowo(y + 2), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
     T x[V];
 #pragma unroll
@@ -1311,6 +1325,43 @@ static inline int pick_rb(int B, int nstrips, int rows, int maxrb = kRB) {
   return 2;
 }
 
+static int num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// Row tasks of the compute-heavier row-pair kernels (sweep+restriction, cycle join), whose 4-wave
+// workgroups run a few per CU at once: choose the task height so the workgroup count fills the CUs
+// evenly (ceil(WGs / CUs) decides the slowest CU), counting the `halo` rows each task re-streams,
+// with at least target_waves() waves in flight.  e.g. 4097^2 fp64: 504 workgroups of 74 rows
+// (2 per CU) instead of 576 of 64 (2.25 per CU: a quarter of the CUs run 3).  FEANET_BALANCE=0
+// restores the power-of-two choice (A/B).  Results are bitwise independent of the task height.
+static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
+  const char* e = getenv("FEANET_BALANCE");
+  if ((e && atoi(e) == 0) || rows_c < 2) return rb_pow2;
+  const long long ncu = num_cus(), nsg = div_up(nstrips, kWaves);
+  const long long min_wg = std::max<long long>(1, target_waves() / kWaves);
+  long long best_cost = -1;
+  int best = rb_pow2;
+  for (int rbc = 1; rbc <= rows_c && 2 * rbc <= 4 * rb_pow2; ++rbc) {
+    const long long ntr = div_up(rows_c, rbc), wgs = (long long)B * ntr * nsg;
+    if (wgs < min_wg) break;  // larger tasks only lower the count further
+    const long long cost = div_up(wgs, ncu) * (2 * rbc + halo);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = 2 * rbc;
+    }
+  }
+  return best;
+}
+
 // Levels whose fields exceed this many bytes stream their stores past the caches (measured on the
 // 4097^2 fp64 sweep: 64.8 us with nontemporal stores vs 84.6 us without)
 static long long nt_bytes() {
@@ -1465,7 +1516,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
     g.bsc = bsc;                                                                                             \
     g.nstrips = div_up(W - 2, Ovl<T>::S);  /* overlapped strips */                                           \
-    g.rb = pick_rb(B, g.nstrips, H - 2, 2 * kRB);                                                            \
+    g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 3, pick_rb(B, g.nstrips, H - 2, 2 * kRB));                    \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
@@ -1528,7 +1579,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;     \
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     g.nstrips = div_up(W - 2, Ovl3<T>::S);                                                                   \
-    g.rb = pick_rb(B, g.nstrips, H - 2, join_max_rb());                                                      \
+    g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 7, pick_rb(B, g.nstrips, H - 2, join_max_rb()));             \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \

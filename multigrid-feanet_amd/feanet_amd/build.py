@@ -30,22 +30,26 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
+def build(force=False, verbose=True, out=None, defines=()):
+    """out / defines: A/B variant libraries for tools/ (loaded with FEANET_LIB_OVERRIDE)."""
+    if out is None and not force and not needs_build():
         return LIB
+    target = out or LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     # -ffp-contract=on: a*b+c is fused only within one source expression, so a value recomputed
     # at a different call site (task-edge rows, edge lanes) rounds identically -> results are
     # independent of rows-per-task and batch size (bitwise)
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-ffp-contract=on", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-pass-failed", f"-I{INCLUDE}", f"-I{CSRC}", *sources(), "-o", LIB + ".tmp"]
+           "-Wno-pass-failed", *[f"-D{d}" for d in defines], f"-I{INCLUDE}", f"-I{CSRC}", *sources(),
+           "-o", target + ".tmp"]
     if verbose:
         print("[feanet_amd.build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    print(LIB)
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
+    outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
+    print(build(force="--force" in sys.argv, out=outs[0] if outs else None, defines=defs))
