@@ -200,7 +200,8 @@ int fea_mg_sweep_f64(const double* u, const double* f, double* out, const uint8_
 /* Fused residual + restriction: fc(interior) = w0 * R(f - K u), kernel by fine-node pattern.
  * u == NULL: zero-initial-guess mode — the kernel first forms v = omd*f (the coarse-level
  * pre-smooth), writes it to v_out, and restricts f - K v (one read of f for three ops:
- * FEANet/multigrid.py:171-172 then :168-170).  (ldc, bstridec) = coarse layout. */
+ * FEANet/multigrid.py:171-172 then :168-170).  v_out may be NULL: v is then not stored (the
+ * prolongation recomputes it, fea_mg_prolong_sweep with u == NULL).  (ldc, bstridec) = coarse layout. */
 int fea_mg_residual_restrict_f32(const float* u, const float* f, float* v_out, float* fc, const uint8_t* pid,
                                  const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
                                  float w0, int B, int H, int W, int ld, long long bstride, int ldc,
@@ -224,7 +225,9 @@ int fea_mg_sweep_restrict_f64(const double* u, const double* f, double* u_out, d
 
 /* Fused prolongation + correction + post-sweep:
  *   out = J(u + w1 * P(ec), f)   (P kernel by coarse-node pattern pidc)
- * FEANet/multigrid.py:177-181 (Interpolate, add, Relax) in one pass. */
+ * FEANet/multigrid.py:177-181 (Interpolate, add, Relax) in one pass.
+ * u == NULL: the level's iterate is its zero-guess pre-sweep omd*f (interior; 0 on the boundary),
+ * recomputed from f — bitwise the v that fea_mg_residual_restrict(u = NULL) would have stored. */
 int fea_mg_prolong_sweep_f32(const float* u, const float* ec, const float* f, float* out, const uint8_t* pid,
                              const uint8_t* pidc, const float* ktab, const float* omd, int ntab,
                              const float* ptab, int nptab, float w1, int B, int H, int W, int ld, long long bstride,

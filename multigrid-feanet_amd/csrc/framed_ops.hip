@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   const long long boff = (long long)id.b * g.bs + poff;
   const T* __restrict__ ub = ZERO ? nullptr : g.u + boff;
   const T* __restrict__ fb = g.f + boff;
-  T* __restrict__ vb = ZERO ? g.out2 + boff : nullptr;
+  T* __restrict__ vb = (ZERO && g.out2) ? g.out2 + boff : nullptr;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + poff : nullptr;
   const int ld = g.ld;
   const int bc0 = (c0 + 1) / 2;  // coarse column of lane 0's first output
@@ -470,6 +470,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   };
   auto store_v = [&](int y, const WRow& w) {
     if constexpr (ZERO) {
+      if (!vb) return;  // v not kept: the prolongation recomputes it from f (k_mg_prolong ZU)
       const bool own = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
       if (own) {
         T o[V];
@@ -752,6 +753,9 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
 // ---------------------------------------------------------------------------
 // Kernel C: fused prolongation + correction (+ post-sweep):
 //   v = u + w1 * P(ec)   (P kernel of the coarse node);   out = SWEEP ? J(v, f) : v
+// ZU (with SWEEP): the level's iterate is its zero-guess pre-sweep u = omd*f (interior, 0 on the
+// boundary) — recomputed from the f rows the sweep reads anyway instead of being stored by the
+// restriction and re-read here (bitwise the same product; 16 B per node less traffic in fp64).
 // ---------------------------------------------------------------------------
 template <typename T, int V>
 struct CRow {  // coarse row at coarse columns b_base-1 .. b_base+V/2 (V/2+2 values)
@@ -829,8 +833,9 @@ __device__ __forceinline__ void correct_odd(Row<T, V>& u, const CRow<T, V>& ca, 
   }
 }
 
-template <typename T, bool MULTI, bool SWEEP, bool NT>
+template <typename T, bool MULTI, bool SWEEP, bool NT, bool ZU = false>
 __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
+  static_assert(!ZU || SWEEP, "ZU needs the sweep's f rows");
   using F = Frame<T>;
   constexpr int V = F::VEC;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
@@ -862,10 +867,17 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const int ld = g.ld, ldc = g.ldc;
   const long long poff = F::OFF + c0;
   const long long boff = (long long)id.b * g.bs + poff;
-  const T* __restrict__ ub = g.u + boff;
   const T* __restrict__ fb = SWEEP ? g.f + boff : nullptr;
+  const T* __restrict__ ub = ZU ? fb : g.u + boff;
   T* __restrict__ ob = g.out + boff;
   const uint8_t* __restrict__ pb = (MULTI && SWEEP) ? g.pid + poff : nullptr;
+  // ZU: interior mask of the lane's window columns
+  bool cin[V + 3];
+#pragma unroll
+  for (int j = 0; j < V + 3; ++j) {
+    const int c = cl + j - 1;
+    cin[j] = c >= 1 && c <= W - 2;
+  }
   const int bc0 = (c0 + 1) / 2;
   const long long pcoff = F::OFF + bc0;
   const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + pcoff;
@@ -886,7 +898,22 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
     return p;
   };
   auto rf = [&](int y, T (&fv)[V]) {
-    if constexpr (SWEEP) vload<T, V>(fb + rowo(y) + V * lane, fv);
+    if constexpr (SWEEP && !ZU) vload<T, V>(fb + rowo(y) + V * lane, fv);
+  };
+  // window row of the iterate from a loaded row: u itself, or (ZU) omd*f with f's own columns kept
+  auto mk = [&](const RawRow<T, V>& raw, int y, const PRow<V>& p, T (&fo)[V]) {
+    Row<T, V> r = finish(raw);
+    if constexpr (ZU) {
+      const bool rin = y >= 1 && y <= H - 2;
+#pragma unroll
+      for (int k = 0; k < V; ++k) fo[k] = r.a[k + 1];
+#pragma unroll
+      for (int j = 0; j < V + 3; ++j) {
+        const T omj = MULTI ? tab[p.a[j] + 9] : om;
+        r.a[j] = (rin && cin[j]) ? omj * r.a[j] : T(0);
+      }
+    }
+    return r;
   };
   auto emit = [&](int y, const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
                   const PRow<V>& pbb, const PRow<V>& pc, const T (&fv)[V]) {
@@ -909,15 +936,15 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   const int a0 = (r0 - 1) / 2;
   CRow<T, V> C0 = finish_c<T, V, MULTI>(rc(a0));
   CRow<T, V> C1 = finish_c<T, V, MULTI>(rc(a0 + 1));
-  Row<T, V> Vp = finish(ru(r0 - 1)), Vc = finish(ru(r0));
+  PRow<V> Pp = fp(rp(r0 - 1)), Pc = fp(rp(r0));
+  T fq[V], f0[V], f1[V];  // ZU: f's own columns of rows r0-1 (unused), r0 (f0), r0+1 (f1)
+  Row<T, V> Vp = mk(ru(r0 - 1), r0 - 1, Pp, fq), Vc = mk(ru(r0), r0, Pc, f0);
   correct_even<T, V, MULTI>(Vp, C0, w1, ps, ptb);
   correct_odd<T, V, MULTI>(Vc, C0, C1, w1, ps, ptb);
-  PRow<V> Pp = fp(rp(r0 - 1)), Pc = fp(rp(r0));
   // prefetched for the first iteration: fine rows r0+1, r0+2, coarse row a0+2, f rows r0, r0+1
   RawRow<T, V> nU1 = ru(r0 + 1), nU2 = ru(r0 + 2);
   RawC<T, V> nC = rc(a0 + 2);
   RawP<V> nP1 = rp(r0 + 1), nP2 = rp(r0 + 2);
-  T f0[V], f1[V];
   rf(r0, f0);
   rf(r0 + 1, f1);
   for (int y = r0; y < r1; y += 2) {
@@ -929,16 +956,16 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
     rf(y + 2, g0);
     rf(y + 3, g1);
     // row y+1 (even, coarse (y+1)/2 = C1)
-    Row<T, V> Vn = finish(nU1);
-    correct_even<T, V, MULTI>(Vn, C1, w1, ps, ptb);
     const PRow<V> Pn = fp(nP1);
+    Row<T, V> Vn = mk(nU1, y + 1, Pn, f1);
+    correct_even<T, V, MULTI>(Vn, C1, w1, ps, ptb);
     emit(y, Vp, Vc, Vn, Pp, Pc, Pn, f0);
     if (y + 1 < r1) {
       // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
       const CRow<T, V> C2 = finish_c<T, V, MULTI>(nC);
-      Row<T, V> Vnn = finish(nU2);
-      correct_odd<T, V, MULTI>(Vnn, C1, C2, w1, ps, ptb);
       const PRow<V> Pnn = fp(nP2);
+      Row<T, V> Vnn = mk(nU2, y + 2, Pnn, g0);
+      correct_odd<T, V, MULTI>(Vnn, C1, C2, w1, ps, ptb);
       emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn, f1);
       Vp = Vn;
       Vc = Vnn;
@@ -954,7 +981,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       f0[k] = g0[k];
-      f1[k] = g1[k];
+      if constexpr (!ZU) f1[k] = g1[k];
     }
   }
 }
@@ -1363,10 +1390,12 @@ static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
 }
 
 // Levels whose fields exceed this many bytes stream their stores past the caches (measured on the
-// 4097^2 fp64 sweep: 64.8 us with nontemporal stores vs 84.6 us without)
+// 4097^2 fp64 sweep: 64.8 us with nontemporal stores vs 84.6 us without).  64 MiB: the three fields
+// of a 2049^2 fp64 level (~36 MB each) stay in the 256 MiB Infinity Cache between the level's
+// restriction and prolongation (V-cycle 201 -> 196 us with 64 instead of 32 MiB, A/B on MI355X).
 static long long nt_bytes() {
   const char* e = getenv("FEANET_NT_BYTES");
-  return e ? atoll(e) : (32ll << 20);
+  return e ? atoll(e) : (64ll << 20);
 }
 
 // rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
@@ -1439,6 +1468,12 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     else K<TARGS, false><<<grid, 256, 0, s>>>(g);                 \
   }
 
+#define FEA_NT_LAUNCH_ZU(K, TARGS)                                \
+  {                                                               \
+    if (g.nt) K<TARGS, true, true><<<grid, 256, 0, s>>>(g);       \
+    else K<TARGS, false, true><<<grid, 256, 0, s>>>(g);           \
+  }
+
 #define FEA_MG_API(SUF, T)                                                                                   \
   extern "C" int fea_mg_pack_##SUF(const T* src, T* dst, const T* geo, long long geo_bs, const T* bc,         \
                                    long long bc_bs, int B, int H, int W, int ld, long long bs, void* stream) { \
@@ -1481,7 +1516,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
     if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;                                                      \
-    if (!u && (!v_out || !omd)) return FEA_EINVAL;                                                           \
+    if (!u && !omd) return FEA_EINVAL;                                                                       \
     MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.out = fc; g.out2 = v_out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;     \
     g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
@@ -1528,7 +1563,9 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
                               const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab,      \
                               int nptab, T w1, int B, int H, int W, int ld, long long bs, int ldc,           \
                               long long bsc, void* stream, bool sweep) {                                     \
-    if (!u || !ec || !out || !ptab || B <= 0 || !layout_ok<T>(H, W, ld, bs) || out == u) return FEA_EINVAL;   \
+    if ((!u && !sweep) || !ec || !out || !ptab || B <= 0 || !layout_ok<T>(H, W, ld, bs) || out == u)         \
+      return FEA_EINVAL;                                                                                     \
+    if (!u && out == f) return FEA_EINVAL;                                                                   \
     if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (nptab < 1 || nptab > FEA_MAX_PATTERNS || (nptab > 1 && !pidc)) return FEA_EINVAL;                    \
     if (sweep && (!f || !ktab || !omd || ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)))          \
@@ -1541,7 +1578,10 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.ldc = ldc; g.bsc = bsc;                                                                                \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (sweep) {                                                                                             \
+    if (sweep && !u) {                                                                                       \
+      if (multi) FEA_NT_LAUNCH_ZU(k_mg_prolong, T COMMA true COMMA true)                                     \
+      else FEA_NT_LAUNCH_ZU(k_mg_prolong, T COMMA false COMMA true)                                          \
+    } else if (sweep) {                                                                                      \
       if (multi) FEA_NT_LAUNCH(k_mg_prolong, T COMMA true COMMA true)                                        \
       else FEA_NT_LAUNCH(k_mg_prolong, T COMMA false COMMA true)                                             \
     } else {                                                                                                 \

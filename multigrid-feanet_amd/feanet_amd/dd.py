@@ -129,6 +129,8 @@ def simulate_validity(program, Ld, ghost, init=None):
     def get(l, name):
         if name is None or name == "zero":
             return INF
+        if name == "omdf":  # omd*f recomputed pointwise: valid where f is
+            return get(l, "f")
         if name == "f" and l == 0:
             return g[0]
         return v.get((l, name), g[l])

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import hjac_schedule, vcycle_schedule
+from .schedule import OMDF, hjac_schedule, vcycle_schedule
 
 
 class _Level:
@@ -310,6 +310,8 @@ class MultigridSolver:
 
     # ------------------------------------------------------------------ schedule
     def _ptr(self, lvl, name):
+        if name == OMDF:  # recomputed in the kernel (u = NULL)
+            return None
         return self.levels[lvl].buf(name).data_ptr()
 
     def _build(self, start):
@@ -515,13 +517,13 @@ class MultigridSolver:
             if name == "mg_sweep":
                 total += nodes * (esz * (3 if args[0] is not None else 2) + pb)
             elif name == "mg_residual_restrict":
-                total += nodes * (esz * (2 if args[0] is not None else 2) + pb) + coarse * esz
-                if args[0] is None:
+                total += nodes * (esz * (2 if args[0] is not None else 1) + pb) + coarse * esz
+                if args[0] is None and args[2] is not None:
                     total += nodes * esz  # v written
             elif name == "mg_sweep_restrict":
                 total += nodes * (3 * esz + pb) + coarse * esz
-            elif name == "mg_prolong_sweep":
-                total += nodes * (3 * esz + pb) + coarse * (esz + pb)
+            elif name == "mg_prolong_sweep":  # u = NULL: the iterate is recomputed from f
+                total += nodes * ((3 if args[0] is not None else 2) * esz + pb) + coarse * (esz + pb)
             elif name == "mg_prolong_add":
                 total += nodes * 2 * esz + coarse * (esz + pb)
         return total

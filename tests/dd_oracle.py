@@ -65,7 +65,8 @@ class OracleRank:
                 b[l][st[3]] = v
             elif st[2] is None:
                 v = self.sweep(l, b[l]["zero"], b[l]["f"])
-                b[l][st[3]] = v
+                if st[3] is not None:
+                    b[l][st[3]] = v
             else:
                 v = b[l][st[2]]
             r = b[l]["f"] - lv[l].K(v)
@@ -76,7 +77,7 @@ class OracleRank:
         elif kind == "prolong_sweep":
             # the kernel's semantics: the corrected field x enters the stencil on every row (also the
             # slab's local edge rows), interior nodes are swept, edge rows keep the source values
-            src = b[l][st[2]]
+            src = self.sweep(l, b[l]["zero"], b[l]["f"]) if st[2] == "omdf" else b[l][st[2]]
             x = src + orc.prolong(b[l + 1][st[3]], lv[l + 1].pid, self.R)
             omd = orc.omega_over_d(lv[l].ktab, 2. / 3., np.float64)[0]
             swept = omd * (b[l]["f"] - lv[l].K(x)) + x

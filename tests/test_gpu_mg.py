@@ -172,6 +172,29 @@ def test_mg_transfer(T, problem, learned, n, B):
     out = fr.get("b")
     close(out[:, 1:-1, 1:-1], ref[:, 1:-1, 1:-1], T, "prolong+sweep")
     assert (out[:, 0, :] == 7).all() and (out[:, :, -1] == 7).all()
+    # recompute mode: RR without storing v, then prolong+sweep with u = NULL (v = omd*f recomputed)
+    # is bitwise the stored-v pair
+    fr.put("a", u * 0)
+    _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), fr.L.a.data_ptr(), co.L.f.data_ptr(), fr.pid(),
+              kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    fc_stored = co.get("f")
+    _lib.call("mg_prolong_sweep", T, fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(),
+              fr.pid(), co.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, w1, *fr.args(), co.L.ld,
+              co.L.bs, None)
+    ps_stored = fr.get("b")
+    co.put("f", fc_stored * 0 + 3.0)
+    fr.put("b", u * 0 + 7.0)
+    _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), None, co.L.f.data_ptr(), fr.pid(),
+              kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, w0, *fr.args(), co.L.ld, co.L.bs, None)
+    assert (fr.get("b") == 7).all(), "v written although v_out = NULL"
+    assert np.array_equal(co.get("f")[:, 1:-1, 1:-1], fc_stored[:, 1:-1, 1:-1])
+    _lib.call("mg_prolong_sweep", T, None, co.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(),
+              fr.pid(), co.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, w1, *fr.args(), co.L.ld,
+              co.L.bs, None)
+    out = fr.get("b")
+    assert np.array_equal(out[:, 1:-1, 1:-1], ps_stored[:, 1:-1, 1:-1]), "recomputed iterate differs"
+    assert (out[:, 0, :] == 7).all() and (out[:, :, -1] == 7).all()
+    fr.put("a", u)
     _lib.call("mg_prolong_add", T, fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.b.data_ptr(), co.pid(), pt.data_ptr(),
               nt, w1, *fr.args(), co.L.ld, co.L.bs, None)
     close(fr.get("b")[:, 1:-1, 1:-1], x[:, 1:-1, 1:-1], T, "prolong+add")

@@ -22,6 +22,8 @@ def interpret(mg, steps, v, f, compat=None):
     def get(l, name):
         if name == "zero":
             return np.zeros((B, lv[l].H, lv[l].W), dt)
+        if name == "omdf":  # zero-guess pre-sweep recomputed from f_l
+            return lv[l].sweep(np.zeros((B, lv[l].H, lv[l].W), dt), fs[l])
         return bufs[l][name]
 
     for st in steps:
@@ -32,7 +34,8 @@ def interpret(mg, steps, v, f, compat=None):
         elif kind == "resid_restrict":
             if st[2] is None:
                 src = lv[l].sweep(np.zeros((B, lv[l].H, lv[l].W), dt), fs[l])
-                bufs[l][st[3]] = src
+                if st[3] is not None:
+                    bufs[l][st[3]] = src
             else:
                 src = get(l, st[2])
             r = fs[l] - lv[l].K(src)
@@ -156,6 +159,11 @@ def test_schedule_shape_and_buffers():
     # 2 coarsest sweeps, 11 fused prolong+sweep
     assert kinds.count("sweep_restrict") == 1 and kinds.count("resid_restrict") == 10
     assert kinds.count("sweep") == 2 and kinds.count("prolong_sweep") == 11 and end == "a"
+    # coarse levels keep no iterate between restriction and prolongation (recomputed omd*f)
+    assert ("resid_restrict", 1, None, None) in steps
+    assert [s[2] for s in steps if s[0] == "prolong_sweep"] == ["omdf"] * 10 + ["b"]
+    steps, end = vcycle_schedule(12, 1, 1, recompute=False)
+    assert ("resid_restrict", 1, None, "a") in steps and "omdf" not in [s[2] for s in steps]
     steps, end = vcycle_schedule(12, 1, 1, fuse=False)
     kinds = [s[0] for s in steps]
     assert kinds.count("sweep") == 3 and kinds.count("resid_restrict") == 11
