@@ -302,6 +302,31 @@ int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Ht, int Wt, int n
 /* LDS bytes the coarse tail needs for (Ht, Wt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
 size_t fea_mg_coarse_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi);
 
+/* Several consecutive coarse levels in ONE launch (mid_ops.hip; tiles with recomputed halos, bitwise
+ * the per-level kernels).  Levels a .. a+k (k <= 4) are framed buffers (fea_mg_layout) of H x W,
+ * (H+1)/2 x (W+1)/2, ...; pid[j] their pattern maps (NULL array when ntab == 1).
+ * mid_down: the zero-guess pre-sweep + residual + restriction of levels a .. a+k-1 (V(1,1) down leg,
+ *   FEANet/multigrid.py:171-172 then :168-170, one fea_mg_residual_restrict(u = NULL) per level):
+ *   reads f[0] = f_a, writes f[1..k] = f_{a+1} .. f_{a+k} (interior).  Tile TR x TC of level a+k.
+ * mid_up: the prolongation + correction + post-sweep of levels a+k-1 .. a from e = u_{a+k}
+ *   (:177-181, one fea_mg_prolong_sweep(u = NULL) per level): reads f[0..k-1] = f_a .. f_{a+k-1},
+ *   writes out = u_a (interior); intermediate iterates are not stored.  Tile TR x TC of level a.
+ * Both return FEA_EINVAL if the tile's LDS footprint (fea_mg_mid_lds_bytes) does not fit. */
+int fea_mg_mid_down_f32(const float* const* f, const uint8_t* const* pid, int k, int B, int H, int W,
+                        const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab, float w0,
+                        int TR, int TC, void* stream);
+int fea_mg_mid_down_f64(const double* const* f, const uint8_t* const* pid, int k, int B, int H, int W,
+                        const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab, double w0,
+                        int TR, int TC, void* stream);
+int fea_mg_mid_up_f32(const float* const* f, const float* e, float* out, const uint8_t* const* pid, int k, int B,
+                      int H, int W, const float* ktab, const float* omd, int ntab, const float* ptab, int nptab,
+                      float w1, int TR, int TC, void* stream);
+int fea_mg_mid_up_f64(const double* const* f, const double* e, double* out, const uint8_t* const* pid, int k,
+                      int B, int H, int W, const double* ktab, const double* omd, int ntab, const double* ptab,
+                      int nptab, double w1, int TR, int TC, void* stream);
+/* LDS bytes of one mid launch (up = 0 down, 1 up) with a full TR x TC tile; -1 if it does not fit. */
+long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi);
+
 #ifdef __cplusplus
 }
 #endif

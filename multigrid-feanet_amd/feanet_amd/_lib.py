@@ -47,12 +47,16 @@ _SIGS = {
     "mg_cycle_join": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", "S", I, I, I, I, LL, I, LL, P],
     "mg_hsweep": [P, P, P, P, P, P, P, I, P, I, I, I, I, I, LL, P],
     "mg_coarse_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
+    # several coarse levels per launch (pointer arrays: ptr_array())
+    "mg_mid_down": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
+    "mg_mid_up": [P, P, P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
 }
 _EXTRA = {
     "fea_abi_version": ([], I),
     "fea_mg_layout": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
     "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
+    "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
     "fea_stencil_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
     "fea_stencil_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
     "fea_transfer_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
@@ -99,7 +103,7 @@ def call(name, dtype, *args):
     if suf is None:
         raise TypeError(f"feanet_amd: unsupported dtype {dtype} (float32/float64 only)")
     fn = getattr(lib(), f"fea_{name}_{suf}")
-    rc = fn(*args)
+    rc = fn(*[a.ptr if isinstance(a, PtrArray) else a for a in args])
     if rc != 0:
         what = "invalid arguments" if rc == -1 else f"hipError_t {rc}"
         raise RuntimeError(f"feanet_amd: fea_{name}_{suf} failed ({what})")
@@ -127,6 +131,22 @@ def weight_grad_ws_bytes(C, B, Hc, Wc):
 
 def stencil_grad_ws_bytes(ntab, B, H, W):
     return int(lib().fea_stencil_weight_grad_ws_bytes_f64(ntab, B, H, W))
+
+
+def mid_lds_bytes(up, k, TR, TC, elem_size, multi):
+    return int(lib().fea_mg_mid_lds_bytes(int(bool(up)), k, TR, TC, elem_size, int(bool(multi))))
+
+
+class PtrArray:
+    """A C array of device pointers (const T* const*) for the mid-level entry points; keeps the
+    ctypes array alive as long as the launch plan that holds it."""
+
+    def __init__(self, ptrs):
+        self.arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        self.ptr = ctypes.cast(self.arr, ctypes.c_void_p).value
+
+    def __repr__(self):
+        return f"PtrArray({list(self.arr)})"
 
 
 def norm_workspace_bytes(B, H, W):

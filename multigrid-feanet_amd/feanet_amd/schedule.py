@@ -17,6 +17,11 @@ Steps:
   ("prolong_add", l, src, csrc, dst)   dst = src + w1 P(v_{l+1}[csrc])
   ("coarse_tail", t, dst)              levels t..L-1 in one launch (coarse_tail.hip): from f_t and a
                                        zero guess, the coarse part of this same schedule; v_t -> dst
+  ("mid_down", a, k, T)                the zero-guess resid_restrict steps of levels a..a+k-1 (vout
+                                       None) in one launch (mid_ops.hip, tile T of level a+k)
+  ("mid_up", a, k, csrc, dst, T)       the "omdf" prolong_sweep steps of levels a+k-1..a in one
+                                       launch: u_a[dst] from u_{a+k}[csrc] (tile T of level a)
+                                       (group_mid rewrites a schedule into these)
 
 Semantics reproduced:
   * nu1 = nu2 = 1: MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372) == MultiGrid.iterate
@@ -168,3 +173,59 @@ def hjac_schedule(L, nu1=1, nu2=1, start="a"):
         for _ in range(nu2):
             hs(l)
     return steps, cur[0]
+
+
+def group_mid(steps, pick_down, pick_up):
+    """Rewrite runs of consecutive zero-guess restrictions (("resid_restrict", l, None, None), l
+    ascending) and of recomputed prolongations (("prolong_sweep", l, OMDF, csrc, dst), l descending)
+    into multi-level launches.  pick_down(levels) / pick_up(levels) get the run's levels (ascending)
+    and return [(a, k, T), ...]: disjoint groups of consecutive levels (a .. a+k-1, k >= 2) with the
+    tile size; levels left out keep their single-level step."""
+    out = []
+    i = 0
+    n = len(steps)
+    while i < n:
+        st = steps[i]
+        if st[0] == "resid_restrict" and st[2] is None and st[3] is None:
+            j = i
+            while (j + 1 < n and steps[j + 1][0] == "resid_restrict" and steps[j + 1][2] is None
+                   and steps[j + 1][3] is None and steps[j + 1][1] == steps[j][1] + 1):
+                j += 1
+            run = steps[i:j + 1]
+            groups = {a: (k, T) for a, k, T in pick_down([s_[1] for s_ in run])}
+            m = 0
+            while m < len(run):
+                l = run[m][1]
+                if l in groups:
+                    k, T = groups[l]
+                    out.append(("mid_down", l, k, T))
+                    m += k
+                else:
+                    out.append(run[m])
+                    m += 1
+            i = j + 1
+            continue
+        if st[0] == "prolong_sweep" and st[2] == OMDF:
+            j = i
+            while (j + 1 < n and steps[j + 1][0] == "prolong_sweep" and steps[j + 1][2] == OMDF
+                   and steps[j + 1][1] == steps[j][1] - 1):
+                j += 1
+            run = steps[i:j + 1]  # levels descending
+            by_level = {s_[1]: s_ for s_ in run}
+            groups = {a: (k, T) for a, k, T in pick_up(sorted(by_level))}
+            m = 0
+            while m < len(run):
+                l = run[m][1]
+                a = next((a_ for a_, (k_, _) in groups.items() if a_ + k_ - 1 == l), None)
+                if a is not None:
+                    k, T = groups[a]
+                    out.append(("mid_up", a, k, by_level[a + k - 1][3], by_level[a][4], T))
+                    m += k
+                else:
+                    out.append(run[m])
+                    m += 1
+            i = j + 1
+            continue
+        out.append(st)
+        i += 1
+    return out

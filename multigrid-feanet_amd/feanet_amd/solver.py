@@ -17,12 +17,13 @@ pointers) and replayed as a HIP graph.  Everything stays on the device; the only
 are the ones a caller asks for (e.g. `.item()` on the residual norm, as the reference drivers do).
 """
 import math
+import os
 
 import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import OMDF, hjac_schedule, vcycle_schedule
+from .schedule import OMDF, group_mid, hjac_schedule, vcycle_schedule
 
 
 class _Level:
@@ -99,12 +100,19 @@ class MultigridSolver:
         join_cycles: vcycle(k) with k >= 2 runs the finest level's post-smooth of each cycle and the
             pre-smooth + residual + restriction of the next as one pass (fea_mg_cycle_join; bitwise
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
+        mid: run latency-bound coarse levels (B*H*W <= MID_NODES) up to four per launch
+            (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels); env FEANET_MID=0 disables.
     """
+
+    MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
+    #                       streaming kernels win: tools/lab/mid_lab.py)
+    MID_MIN_TILES = 200   # workgroups a multi-level launch should give the 256 CUs
+    MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None, join_cycles=True):
+                 smoother="jac", hnet=None, join_cycles=True, mid=True):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -136,6 +144,7 @@ class MultigridSolver:
         self.fuse = fuse
         self.zero_start = zero_start
         self.join_cycles = join_cycles
+        self.mid = bool(mid) and os.environ.get("FEANET_MID", "1") != "0"
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -322,7 +331,52 @@ class MultigridSolver:
         else:
             steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
                                          top_zero=self.zero_start)
+            if self.mid:
+                steps = group_mid(steps, lambda lv: self._pick_mid(lv, False), lambda lv: self._pick_mid(lv, True))
         return [self.bind_step(st) for st in steps], end
+
+    def _mid_tile(self, up, a, k):
+        """Tile size for a multi-level launch over levels a..a+k-1 (down: tile of level a+k; up: of
+        level a), or None: the largest power of two whose LDS footprint fits, that gives the chip
+        >= MID_MIN_TILES workgroups (or the most it can) and, going down, stages <= MID_MAX_REDUNDANCY
+        times the top level's nodes."""
+        esz = 4 if self.dtype == torch.float32 else 8
+        multi = self.ntab > 1
+        tl = self.levels[a if up else a + k]
+        top = self.levels[a]
+        best = None
+        for T in ((128, 64, 32, 16, 8) if up else (32, 16, 8, 4, 2)):
+            if _lib.mid_lds_bytes(up, k, T, T, esz, multi) <= 0:
+                continue
+            tiles = self.B * -(-(tl.H - 2) // T) * -(-(tl.W - 2) // T)
+            if not up:
+                reg = (T << k) + 3 * ((1 << k) - 1)
+                if reg * reg * tiles > self.MID_MAX_REDUNDANCY * self.B * top.H * top.W:
+                    continue
+            best = T
+            if tiles >= self.MID_MIN_TILES:
+                return T
+        return best
+
+    def _pick_mid(self, levels, up):
+        """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
+        el = sorted(l for l in levels
+                    if self.B * self.levels[l].H * self.levels[l].W <= self.MID_NODES and l + 1 < self.L)
+        groups = []
+        hi = len(el)
+        while hi >= 2:
+            for k in range(min(4, hi), 1, -1):
+                a = el[hi - k]
+                if el[hi - 1] - a != k - 1:
+                    continue
+                T = self._mid_tile(up, a, k)
+                if T:
+                    groups.append((a, k, T))
+                    hi -= k
+                    break
+            else:
+                hi -= 1
+        return groups
 
     def bind_step(self, st):
         """One schedule step -> (C-ABI function base name, args without the stream)."""
@@ -362,6 +416,17 @@ class MultigridSolver:
         if kind == "prolong_add":
             return ("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
                                        self.w[1]) + geom(l) + cgeom(l))
+        if kind == "mid_down":
+            a, k, T = st[1], st[2], st[3]
+            fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + k + 1)])
+            pids = _lib.PtrArray([pid(j) for j in range(a, a + k + 1)]) if nt > 1 else None
+            return ("mg_mid_down", (fs, pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt, rt, nr, self.w[0], T, T))
+        if kind == "mid_up":
+            a, k, csrc, dst, T = st[1:6]
+            fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + k)])
+            pids = _lib.PtrArray([pid(j) for j in range(a, a + k + 1)]) if nt > 1 else None
+            return ("mg_mid_up", (fs, ptr(a + k, csrc), ptr(a, dst), pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt,
+                                  pt, npt, self.w[1], T, T))
         if kind == "coarse_tail":
             t = l
             return ("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
@@ -413,21 +478,30 @@ class MultigridSolver:
             self._graphs[key] = g
         g.replay()
 
-    def _vcycles_joined(self, k):
-        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles)."""
+    def joined_program(self, k):
+        """vcycle(k) with joined cycle boundaries as [(segment key, launches)] plus the end buffer:
+        the first cycle's SR(0), k-1 segments (coarse part + cycle join) and the last coarse part +
+        PS(0).  (Also used by bench.py to time the join kernel inside the cycle.)"""
         other = lambda b: "b" if b == "a" else "a"
         s0 = self._state
         plan, _ = self._plan(s0)
         head, mid = plan[0], plan[1:-1]
         ec_ptr = plan[-1][1][1]  # level-1 correction the finest prolongation reads (same every cycle)
-        self._run_segment(("head", s0), [head])
+        prog = [(("head", s0), [head])]
         pre = other(s0)
         for _ in range(k - 1):
-            self._run_segment(("join", pre), mid + [self._join_call(pre, ec_ptr)])
+            prog.append((("join", pre), mid + [self._join_call(pre, ec_ptr)]))
             pre = other(pre)
         tail = self._plan(other(pre))[0][-1]  # PS(0): pre -> other(pre)
-        self._run_segment(("tail", pre), mid + [tail])
-        self._state = other(pre)
+        prog.append((("tail", pre), mid + [tail]))
+        return prog, other(pre)
+
+    def _vcycles_joined(self, k):
+        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles)."""
+        prog, end = self.joined_program(k)
+        for key, launches in prog:
+            self._run_segment(key, launches)
+        self._state = end
 
     def vcycle(self, k=1):
         """Run k V-cycles on the resident iterate (asynchronous; no host sync)."""
@@ -509,6 +583,17 @@ class MultigridSolver:
         total = 0
         for name, args in plan:
             if name == "mg_coarse_tail":
+                continue
+            if name in ("mg_mid_down", "mg_mid_up"):
+                k, B, H, W = args[4:8] if name == "mg_mid_up" else args[2:6]
+                sizes = []
+                for _ in range(k + 1):
+                    sizes.append(B * (H - 2) * (W - 2))
+                    H, W = (H + 1) // 2, (W + 1) // 2
+                if name == "mg_mid_down":  # read f_a, write f_{a+1..a+k}
+                    total += esz * sum(sizes) + pb * sum(sizes[:-1])
+                else:  # read f_a..f_{a+k-1}, u_{a+k}; write u_a
+                    total += esz * (sum(sizes) + sizes[0]) + pb * sum(sizes)
                 continue
             B, H, W = (args[-7:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",
                                                "mg_sweep_restrict") else args[-5:-2])

@@ -26,7 +26,17 @@ def interpret(mg, steps, v, f, compat=None):
             return lv[l].sweep(np.zeros((B, lv[l].H, lv[l].W), dt), fs[l])
         return bufs[l][name]
 
-    for st in steps:
+    expanded = []
+    for st in steps:  # multi-level launches = their per-level steps (feanet_amd.schedule.group_mid)
+        if st[0] == "mid_down":
+            expanded += [("resid_restrict", l, None, None) for l in range(st[1], st[1] + st[2])]
+        elif st[0] == "mid_up":
+            a, k, csrc, dst = st[1:5]
+            expanded += [("prolong_sweep", l, "omdf", csrc if l == a + k - 1 else "mid", dst if l == a else "mid")
+                         for l in range(a + k - 1, a - 1, -1)]
+        else:
+            expanded.append(st)
+    for st in expanded:
         kind, l = st[0], st[1]
         if kind == "sweep":
             src = np.zeros((B, lv[l].H, lv[l].W), dt) if st[2] is None else get(l, st[2])
@@ -175,3 +185,31 @@ def test_schedule_shape_and_buffers():
     # odd number of fine writes alternates the resident buffer
     steps, end = vcycle_schedule(4, 2, 1)
     assert end == "b"
+
+
+@pytest.mark.parametrize("groups", [[(1, 3)], [(2, 2)], [(1, 2), (3, 2)], [(1, 4)]])
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+def test_mid_grouping_equals_per_level(problem, groups):
+    """group_mid (multi-level launches) is the per-level schedule: same steps once expanded, same
+    V-cycle result with oracle operators, and the grouped steps name the right buffers."""
+    from feanet_amd.schedule import group_mid
+    n, L = 64, 6
+    rng = np.random.default_rng(7)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    mg.nu, mg.q2 = (1, 1), False
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    steps, end = vcycle_schedule(L, 1, 1, tail_from=5)
+    pick = lambda levels: [(a, k, 4) for a, k in groups if set(range(a, a + k)) <= set(levels)]
+    grouped = group_mid(steps, pick, pick)
+    kinds = [s[0] for s in grouped]
+    assert kinds.count("mid_down") == len(groups) and kinds.count("mid_up") == len(groups)
+    for s in grouped:
+        if s[0] == "mid_up":
+            a, k, csrc, dst, T = s[1:]
+            assert dst == "a" and T == 4 and csrc == ("a" if a + k == 5 else "a")
+    ref = interpret(mg, steps, v, f)[0][end]
+    out = interpret(mg, grouped, v, f)[0][end]
+    np.testing.assert_array_equal(out, ref)
+    assert end == "a" or end == "b"
+    np.testing.assert_allclose(out, mg.step(v, f), rtol=1e-13, atol=1e-13)

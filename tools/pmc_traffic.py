@@ -28,6 +28,7 @@ def short(n):
 
 
 def main(fcsv, wcsv, out_json, summary=None, src="profiles/r01_pmc"):
+    """FETCH/WRITE csv: rocprofv3 --pmc counter_collection.csv of the two passes."""
     fetch = load(fcsv, "FETCH_SIZE")
     write = load(wcsv, "WRITE_SIZE")
     rows = []
@@ -37,12 +38,17 @@ def main(fcsv, wcsv, out_json, summary=None, src="profiles/r01_pmc"):
         w = 1024 * sum(write[key]) / len(write[key])
         rows.append((short(name), grid, len(fetch[key]), f, w))
     res = {}
+    nodes, cnodes = 4095 * 4095, 2047 * 2047
     for name, grid, n, f, w in rows:
+        key = alg = None
         if name.startswith("k_mg_sweep<double, false, false") and grid == 262144:
-            nodes = 4095 * 4095
-            res["mg_sweep_f64_4097"] = {
+            key, alg = "mg_sweep_f64_4097", 24 * nodes
+        elif name.startswith("k_mg_cycle_join<double, false") and n >= 10:  # the 4097^2 join (most launches)
+            key, alg = "mg_cycle_join_f64_4097", 24 * nodes + 16 * cnodes
+        if key and (key not in res or res[key]["launches"] < n):
+            res[key] = {
                 "hbm_bytes_per_launch": f + w, "read_bytes_per_launch": f, "write_bytes_per_launch": w,
-                "algorithmic_bytes_per_launch": 24 * nodes, "launches": n,
+                "algorithmic_bytes_per_launch": alg, "launches": n, "grid": grid,
                 "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads), KiB -> bytes",
                 "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({src})"}
     json.dump(res, open(out_json, "w"), indent=1)
