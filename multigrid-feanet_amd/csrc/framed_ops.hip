@@ -1005,6 +1005,17 @@ __device__ __forceinline__ X& pick(X& a, X& b) {
   else return a;
 }
 
+// cycle join: input rows in flight per wave (2 or 4) and the occupancy the register budget is held to
+// (0: the compiler's choice).  A/B on MI355X (tools/lab/ab_bench.sh, V-cycle): 2 rows, free budget
+// (144 VGPRs, 3 waves/SIMD) 196.6 us; 4 rows at 3 waves (spills) 199.3 us; 4 rows at 2 waves 206.0 us.
+#ifndef FEA_JOIN_AHEAD
+#define FEA_JOIN_AHEAD 2
+#endif
+#ifndef FEA_JOIN_WAVES
+#define FEA_JOIN_WAVES 0
+#endif
+static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of 2 or 4 rows");
+
 template <typename T>
 struct Ovl3 {
   static constexpr int V = Frame<T>::VEC;
@@ -1015,7 +1026,12 @@ struct Ovl3 {
 };
 
 template <typename T, bool MULTI, bool NT>
-__global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
+__global__ __launch_bounds__(256)
+#if FEA_JOIN_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(FEA_JOIN_WAVES)))
+#endif
+void k_mg_cycle_join(MgArgs<T> g) {
+  constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
   using F = Frame<T>;
   using O = Ovl3<T>;
   constexpr int V = F::VEC;
@@ -1082,17 +1098,18 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
   for (int q = 0; q < Q; ++q) acc[q] = T(0);
 
   const int ys = 2 * I0 - 4, ye = 2 * I1 + 2;
-  // inputs u(y), f(y-1), pid(y) in flight two steps ahead, in a ping-pong pair of buffers: even steps
-  // consume and refill A, odd steps B, so no in-flight register is ever copied (a copy would force
-  // the wait for its load at once) — the join runs ~2 waves per SIMD and needs the latency cover
-  T uA[V], fA[V], uB[V], fB[V];
-  int pA[V], pB[V];
-  vload<T, V>(ub + rowo(ys), uA);
-  vload<T, V>(fb + rowo(ys - 1), fA);
-  if constexpr (MULTI) pload<V>(pb + rowo(ys), pA);
-  vload<T, V>(ub + rowo(ys + 1), uB);
-  vload<T, V>(fb + rowo(ys), fB);
-  if constexpr (MULTI) pload<V>(pb + rowo(ys + 1), pB);
+  // inputs u(y), f(y-1), pid(y) in flight kJoinAhead steps ahead, in a ring of buffers indexed by the
+  // step's position mod kJoinAhead (compile-time), so no in-flight register is ever copied (a copy
+  // would force the wait for its load at once) — the join runs 3 waves per SIMD and needs the
+  // latency cover: 4 rows x 2 KiB of u and f per wave in flight
+  T ub_[kJoinAhead][V], fb_[kJoinAhead][V];
+  int pb_[kJoinAhead][V];
+#pragma unroll
+  for (int q = 0; q < kJoinAhead; ++q) {
+    vload<T, V>(ub + rowo(ys + q), ub_[q]);
+    vload<T, V>(fb + rowo(ys + q - 1), fb_[q]);
+    if constexpr (MULTI) pload<V>(pb + rowo(ys + q), pb_[q]);
+  }
   CRow<T, V> Ca = finish_c<T, V, MULTI>(rc(ys / 2));
   CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(ys / 2 + 1));
   RawC<T, V> nC = rc(ys / 2 + 2);
@@ -1111,11 +1128,12 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
   };
 
   auto step = [&](int y, auto par) {
-    constexpr int ODD = decltype(par)::value;
-    // this step's inputs; refill the buffer with the rows two steps ahead
-    T(&bu)[V] = pick<ODD>(uA, uB);
-    T(&bf)[V] = pick<ODD>(fA, fB);
-    int(&bp)[V] = pick<ODD>(pA, pB);
+    constexpr int SLOT = decltype(par)::value % kJoinAhead;  // y - ys mod kJoinAhead
+    constexpr int ODD = decltype(par)::value & 1;            // (ys is even)
+    // this step's inputs; refill the slot with the rows kJoinAhead steps ahead
+    T(&bu)[V] = ub_[SLOT];
+    T(&bf)[V] = fb_[SLOT];
+    int(&bp)[V] = pb_[SLOT];
     T u0[V], fy1[V];
     int p0[V];
 #pragma unroll
@@ -1124,9 +1142,9 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
       fy1[k] = bf[k];
       if constexpr (MULTI) p0[k] = bp[k];
     }
-    vload<T, V>(ub + rowo(y + 2), bu);
-    vload<T, V>(fb + rowo(y + 1), bf);
-    if constexpr (MULTI) pload<V>(pb + rowo(y + 2), bp);
+    vload<T, V>(ub + rowo(y + kJoinAhead), bu);
+    vload<T, V>(fb + rowo(y + kJoinAhead - 1), bf);
+    if constexpr (MULTI) pload<V>(pb + rowo(y + kJoinAhead), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
     T x[V];
 #pragma unroll
@@ -1227,12 +1245,18 @@ __global__ __launch_bounds__(256) void k_mg_cycle_join(MgArgs<T> g) {
     }
   };
 
+  // ye - ys + 1 steps (odd); the ring slot is a template argument, so the loop is unrolled by 4 (a
+  // multiple of the ring)
   int y = ys;
-  for (; y < ye; y += 2) {
+  for (; y + 3 <= ye; y += 4) {
     step(y, std::integral_constant<int, 0>{});
     step(y + 1, std::integral_constant<int, 1>{});
+    step(y + 2, std::integral_constant<int, 2>{});
+    step(y + 3, std::integral_constant<int, 3>{});
   }
-  step(y, std::integral_constant<int, 0>{});
+  if (y <= ye) step(y, std::integral_constant<int, 0>{});
+  if (y + 1 <= ye) step(y + 1, std::integral_constant<int, 1>{});
+  if (y + 2 <= ye) step(y + 2, std::integral_constant<int, 2>{});
 }
 
 // ---------------------------------------------------------------------------
