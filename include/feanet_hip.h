@@ -73,6 +73,18 @@ int fea_knet_apply_f64(const double* u, double* y, const uint8_t* pid, const dou
 int fea_split_x_f32(const float* x, float* xs, const uint8_t* pid, int C, int B, int H, int W, void* stream);
 int fea_split_x_f64(const double* x, double* xs, const uint8_t* pid, int C, int B, int H, int W, void* stream);
 
+/* Periodic weighted-Jacobi sweep (JacobiBlockPBC.jacobi_convolution, FEANet/jacobi.py:86-97), period
+ * n = N - 1, single pattern: out (B x N x N) = omd[0] * (f(a+1, b+1) - K u_periodic(a, b)) +
+ * u(a mod n, b mod n); f is the (N+2) x (N+2) forcing term (FNet of the periodic extension). */
+int fea_jacobi_sweep_pbc_f32(const float* u, const float* f, float* out, const float* ktab, const float* omd,
+                             int B, int N, void* stream);
+int fea_jacobi_sweep_pbc_f64(const double* u, const double* f, double* out, const double* ktab,
+                             const double* omd, int B, int N, void* stream);
+/* Circular extension of u[:, :-1, :-1] (period N - 1) to (N - 1 + lo + hi)^2 (lo rows/columns before):
+ * pbc_boundary (jacobi.py:72-79) is lo = 1, hi = 2; reset_boundary (:81-84) is lo = 0, hi = 1. */
+int fea_pbc_pad_f32(const float* u, float* dst, int B, int N, int lo, int hi, void* stream);
+int fea_pbc_pad_f64(const double* u, double* dst, int B, int N, int lo, int hi, void* stream);
+
 /* One weighted-Jacobi sweep, out-of-place:
  *   u0 = u*geo + bc; r = f - K u0; out = (omd[pid]*r + u0)*geo + bc.
  * geo/bc: NULL = square domain (1 inside, 0 on the edge) / zero; *_bstride = elements
@@ -326,6 +338,13 @@ int fea_mg_mid_up_f64(const double* const* f, const double* e, double* out, cons
                       int nptab, double w1, int TR, int TC, void* stream);
 /* LDS bytes of one mid launch (up = 0 down, 1 up) with a full TR x TC tile; -1 if it does not fit. */
 long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi);
+
+/* On-device mesh set-up: the MeshCenterInterface node pattern map — replaces
+ * FEANet/mesh.py place_circle / place_rect (:62-76), identify_patterns (:78-93) and
+ * generate_global_pattern_map (:95-101) with one thread per node, bit-identical to the reference's
+ * float32 geometry.  out[r * ld + c] = pattern id (0..15) of node (r, c), 0 on the boundary;
+ * shape 0 = circle, 1 = square inclusion; size = plate edge length (the reference's `size`). */
+int fea_interface_pattern_map(uint8_t* out, long long ld, int N, int shape, double size, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,4 +1,4 @@
-"""JacobiBlock (reference: FEANet/jacobi.py:5-47) with the sweep as one HIP kernel."""
+"""JacobiBlock / JacobiBlockPBC (reference: FEANet/jacobi.py:5-97) with each sweep as one HIP kernel."""
 import numpy as np
 import torch
 
@@ -46,3 +46,50 @@ class JacobiBlock:
         omd = self._omd.to(device=u.device).to(dt)
         pid = self.Knet._pid(u) if self.Knet.n_channel > 1 else None
         return ops.jacobi_sweep(u, f, kt, omd, pid, geo, bc)
+
+
+class JacobiBlockPBC:
+    """Weighted Jacobi with periodic boundary conditions (FEANet/jacobi.py:50-97; homogeneous meshes).
+
+    Same constructor, attributes (`d_mat` [1,1,N,N] in the default dtype, `omega`, `mesh`, `Knet`) and
+    methods as the reference: pbc_boundary(u) -> [.., N+2, N+2] circular extension, reset_boundary(u)
+    -> [.., N, N] (last row/column = first), jacobi_convolution(u, forcing_term) with the (N+2)^2
+    forcing term of its drivers (f = FNet(pbc_boundary(F))).  Each method is one HIP kernel
+    (fea_pbc_pad, fea_jacobi_sweep_pbc); inputs must be GPU tensors."""
+
+    def __init__(self, mesh, Knet=None, omega=2. / 3.):
+        self.nnode_edge = mesh.nnode_edge
+        self.omega = omega
+        self.mesh = mesh
+        N = self.nnode_edge
+        self.d_mat = torch.zeros((1, 1, N, N))  # compute_diagonal_matrix (:62-70): sum_p mask_p W_p[1,1]
+        for pkey in mesh.kernel_dict:
+            w = torch.from_numpy(np.asarray(mesh.kernel_dict[pkey], np.float32))
+            g = torch.from_numpy(np.asarray(mesh.global_pattern_center[pkey])).reshape(N, N)
+            self.d_mat[0, 0] += g * w[1, 1]
+        self.Knet = Knet
+        if len(mesh.kernel_dict) != 1:
+            raise NotImplementedError("JacobiBlockPBC: homogeneous meshes only (as the reference, jacobi.py:51)")
+        centre = np.float32(np.asarray(mesh.kernel_dict[sorted(mesh.kernel_dict)[0]], np.float32)[1, 1])
+        self._centre = torch.tensor([centre], dtype=torch.float32)
+
+    def pbc_boundary(self, u):
+        """[.., n+1, n+1] -> [.., n+3, n+3] circular extension of u[..., :-1, :-1] (jacobi.py:72-79)."""
+        ops.require_hip(u, "u")
+        return ops.pbc_pad(u, 1, 2)
+
+    def reset_boundary(self, u):
+        """[.., n+1, n+1] -> same size, last row/column copied from the first (jacobi.py:81-84)."""
+        ops.require_hip(u, "u")
+        return ops.pbc_pad(u, 0, 1)
+
+    def jacobi_convolution(self, u, forcing_term):
+        """One periodic sweep (jacobi.py:86-97): omega/d (f - K pbc(u))[1:-1, 1:-1] + reset(u)."""
+        ops.require_hip(u, "u")
+        dt = torch.promote_types(u.dtype, self.d_mat.dtype)
+        u = u.to(dt)
+        kt = (self.Knet._tables(u) if self.Knet is not None
+              else torch.from_numpy(np.asarray(self.mesh.kernel_dict[0], np.float32)).to(u.device, dt))
+        # omega/d_mat in d_mat's dtype as torch evaluates it (reciprocal * omega), then promoted
+        omd = (torch.reciprocal(self._centre.to(self.d_mat.dtype)) * self.omega).to(dt)
+        return ops.jacobi_sweep_pbc(u, forcing_term.to(dt), kt, omd)

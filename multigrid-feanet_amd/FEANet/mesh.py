@@ -77,14 +77,99 @@ class _MeshBase:
             self._points, self._cells = _grid(self.size, self.nnode_edge)
         return self._cells
 
-    def save_mesh(self, outfile):
+    def save_mesh(self, outfile, point_data=None):
+        """VTK export of the quad mesh with its element phases (FEANet/mesh.py:119-120 writes it with
+        meshio).  meshio is used when installed; otherwise a legacy binary VTK file (UNSTRUCTURED_GRID,
+        VTK_QUAD cells, CELL_DATA "Phase") is written directly.  point_data: optional {name: [N*N]}
+        nodal fields (e.g. a solution) — an extension the reference does not have."""
         try:
             import meshio
-        except ImportError as e:  # pragma: no cover
-            raise RuntimeError("save_mesh needs the optional meshio package (VTK export)") from e
-        m = meshio.Mesh(self.points, [("quad", self.cells)])
+        except ImportError:
+            write_vtk_legacy(outfile, self.points, self.cells, {"Phase": self.phase}, point_data or {})
+            return
+        m = meshio.Mesh(self.points, [("quad", self.cells)], point_data=point_data or {})
         m.cell_data["Phase"] = [self.phase]
         m.write(outfile)
+
+
+def write_vtk_legacy(path, points, cells, cell_data, point_data):
+    """Legacy binary VTK (big-endian) of a quad mesh: POINTS float32 x 3, CELLS (4 + ids) int32,
+    CELL_TYPES 9 (VTK_QUAD), scalar CELL_DATA / POINT_DATA fields (int -> int, float -> double)."""
+    pts = np.asarray(points, np.float32).reshape(-1, 3)
+    cl = np.asarray(cells, np.int64).reshape(-1, 4)
+    nc = cl.shape[0]
+    with open(path, "wb") as fh:
+        w = fh.write
+        w(b"# vtk DataFile Version 3.0\nFEANet mesh (feanet_amd)\nBINARY\nDATASET UNSTRUCTURED_GRID\n")
+        w(f"POINTS {pts.shape[0]} float\n".encode())
+        w(pts.astype(">f4").tobytes())
+        w(f"\nCELLS {nc} {5 * nc}\n".encode())
+        conn = np.concatenate([np.full((nc, 1), 4, np.int64), cl], axis=1)
+        w(conn.astype(">i4").tobytes())
+        w(f"\nCELL_TYPES {nc}\n".encode())
+        w(np.full(nc, 9, ">i4").tobytes())
+        w(b"\n")
+
+        def fields(kind, n, data):
+            if not data:
+                return
+            w(f"{kind} {n}\n".encode())
+            for name, v in data.items():
+                v = np.asarray(v).reshape(-1)
+                if v.shape[0] != n:
+                    raise ValueError(f"write_vtk_legacy: field {name!r} has {v.shape[0]} values, expected {n}")
+                if np.issubdtype(v.dtype, np.integer):
+                    w(f"SCALARS {name} int 1\nLOOKUP_TABLE default\n".encode())
+                    w(v.astype(">i4").tobytes())
+                else:
+                    w(f"SCALARS {name} double 1\nLOOKUP_TABLE default\n".encode())
+                    w(v.astype(">f8").tobytes())
+                w(b"\n")
+
+        fields("CELL_DATA", nc, cell_data)
+        fields("POINT_DATA", pts.shape[0], point_data)
+
+
+def read_vtk_legacy(path):
+    """Reader for write_vtk_legacy's files (tests): points, cells, cell_data, point_data."""
+    raw = open(path, "rb").read()
+    pos = 0
+
+    def line():
+        nonlocal pos
+        e = raw.index(b"\n", pos)
+        s_ = raw[pos:e].decode()
+        pos = e + 1
+        return s_
+
+    def block(n, dt):
+        nonlocal pos
+        nb = n * np.dtype(dt).itemsize
+        a = np.frombuffer(raw[pos:pos + nb], dt).copy()
+        pos += nb + 1
+        return a
+
+    for _ in range(4):
+        line()
+    npts = int(line().split()[1])
+    pts = block(3 * npts, ">f4").reshape(-1, 3)
+    nc = int(line().split()[1])
+    conn = block(5 * nc, ">i4").reshape(nc, 5)
+    line()
+    types = block(nc, ">i4")
+    out = {"points": pts, "cells": conn[:, 1:], "types": types, "CELL_DATA": {}, "POINT_DATA": {}}
+    sect = None
+    while pos < len(raw):
+        t = line().split()
+        if not t:
+            continue
+        if t[0] in ("CELL_DATA", "POINT_DATA"):
+            sect, n = t[0], int(t[1])
+            continue
+        name, typ = t[1], t[2]
+        line()  # LOOKUP_TABLE
+        out[sect][name] = block(n, ">i4" if typ == "int" else ">f8")
+    return out
 
 
 class MeshCenterInterface(_MeshBase):

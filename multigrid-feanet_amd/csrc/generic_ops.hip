@@ -105,6 +105,48 @@ __global__ __launch_bounds__(256) void k_jacobi(const T* __restrict__ u, const T
   out[b * HW + i] = reset_at(gb, bb, i, i, u1, r, c, H, W);
 }
 
+// Periodic weighted-Jacobi sweep (JacobiBlockPBC.jacobi_convolution, FEANet/jacobi.py:86-97) on the
+// N x N node grid with period n = N - 1.  The reference extends u circularly to (n+3)^2
+// (pbc_boundary :72-79), convolves with K (zero padding never reaches the kept rows), crops
+// [1:-1, 1:-1] and adds reset_boundary(u) (:81-84, the circular (n+1)^2 copy):
+//   out(a, b) = omd * (f(a+1, b+1) - sum_d W[d] u((a+dy) mod n, (b+dx) mod n)) + u(a mod n, b mod n)
+// with f the (N+2)^2 forcing term the reference's drivers build (FNet of the periodic extension).
+// Single pattern only ("currently only for homogeneous problems", jacobi.py:51).
+template <typename T>
+__global__ __launch_bounds__(256) void k_jacobi_pbc(const T* __restrict__ u, const T* __restrict__ f,
+                                                    T* __restrict__ out, const T* __restrict__ ktab,
+                                                    const T* __restrict__ omd, int N) {
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= N || c >= N) return;
+  const int n = N - 1, M = N + 2;
+  const int b = blockIdx.z;
+  const T* ub = u + (long long)b * N * N;
+  auto wrap = [n](int x) { return x < 0 ? x + n : (x >= n ? x - n : x); };
+  T acc = 0;
+#pragma unroll
+  for (int dr = 0; dr < 3; ++dr) {
+    const long long row = (long long)wrap(r + dr - 1) * N;
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) acc += ktab[dr * 3 + dc] * ub[row + wrap(c + dc - 1)];
+  }
+  const T res = f[(long long)b * M * M + (long long)(r + 1) * M + (c + 1)] - acc;
+  out[(long long)b * N * N + (long long)r * N + c] = omd[0] * res + ub[(long long)wrap(r) * N + wrap(c)];
+}
+
+// Circular extension of the periodic part u[:-1, :-1] (period n = N - 1) to (n + lo + hi)^2:
+// dst(i, j) = u((i - lo) mod n, (j - lo) mod n).  lo = 1, hi = 2: pbc_boundary (jacobi.py:72-79);
+// lo = 0, hi = 1: reset_boundary (:81-84).
+template <typename T>
+__global__ __launch_bounds__(256) void k_pbc_pad(const T* __restrict__ u, T* __restrict__ dst, int N, int lo,
+                                                 int M) {
+  const int c = blockIdx.x * kBX + threadIdx.x, r = blockIdx.y * kBY + threadIdx.y;
+  if (r >= M || c >= M) return;
+  const int n = N - 1;
+  const int b = blockIdx.z;
+  const int sr = ((r - lo) % n + n) % n, sc = ((c - lo) % n + n) % n;
+  dst[(long long)b * M * M + (long long)r * M + c] = u[(long long)b * N * N + (long long)sr * N + sc];
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_residual(const T* __restrict__ u, const T* __restrict__ f,
                                                   T* __restrict__ res, const uint8_t* __restrict__ pid,
@@ -503,6 +545,18 @@ static inline bool bad_shape(int B, int H, int W) { return B <= 0 || H <= 0 || W
     k_jacobi<T><<<grid_for(H, W, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, f, out, pid, ktab, omd, \
                                                                                 ntab, geo, geo_bs, bc,   \
                                                                                 bc_bs, H, W);            \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_jacobi_sweep_pbc_##SUF(const T* u, const T* f, T* out, const T* ktab, const T* omd,  \
+                                            int B, int N, void* stream) {                                \
+    if (!u || !f || !out || !ktab || !omd || out == u || bad_shape(B, N, N)) return FEA_EINVAL;          \
+    k_jacobi_pbc<T><<<grid_for(N, N, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, f, out, ktab, omd, N); \
+    FEA_LAUNCH_CHECK();                                                                                  \
+  }                                                                                                      \
+  extern "C" int fea_pbc_pad_##SUF(const T* u, T* dst, int B, int N, int lo, int hi, void* stream) {     \
+    if (!u || !dst || lo < 0 || hi < 0 || lo + hi > 64 || bad_shape(B, N, N)) return FEA_EINVAL;         \
+    const int M = N - 1 + lo + hi;                                                                       \
+    k_pbc_pad<T><<<grid_for(M, M, B), dim3(kBX, kBY), 0, (hipStream_t)stream>>>(u, dst, N, lo, M);        \
     FEA_LAUNCH_CHECK();                                                                                  \
   }                                                                                                      \
   extern "C" int fea_residual_##SUF(const T* u, const T* f, T* r, const uint8_t* pid, const T* ktab,    \

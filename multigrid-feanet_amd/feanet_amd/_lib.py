@@ -25,6 +25,8 @@ _SIGS = {
     "split_x": [P, P, P, I, I, I, I, P],
     "jacobi_sweep": [P, P, P, P, P, P, I, P, LL, P, LL, I, I, I, P],
     "residual": [P, P, P, P, P, I, I, I, I, P],
+    "jacobi_sweep_pbc": [P, P, P, P, P, I, I, P],
+    "pbc_pad": [P, P, I, I, I, I, P],
     "restrict": [P, I, P, P, P, I, "S", I, I, I, P],
     "prolong": [P, I, P, P, P, P, I, "S", I, I, I, P],
     "residual_norm": [P, P, P, P, I, P, P, I, I, I, P],
@@ -57,6 +59,7 @@ _EXTRA = {
     "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
     "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
+    "fea_interface_pattern_map": ([P, LL, I, I, F64, P], I),
     "fea_stencil_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
     "fea_stencil_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
     "fea_transfer_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),

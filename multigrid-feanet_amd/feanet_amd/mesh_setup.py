@@ -105,3 +105,23 @@ def omega_over_d(ktab, omega, dtype):
 def linear_transfer_kernel():
     """[[1,2,1],[2,4,2],[1,2,1]] float32 (M-FEANet-mg_test.ipynb cell 20 before the /4)."""
     return np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float32)
+
+
+def interface_pattern_map_device(N, shape=0, size=2.0, device="cuda", out=None, ld=None):
+    """interface_pattern_map computed on the GPU (setup_ops.hip, fea_interface_pattern_map): one
+    thread per node, bit-identical to the host restatement / the reference.  Returns a uint8 [N, N]
+    tensor, or writes rows of pitch `ld` bytes into the uint8 tensor `out` starting at its first
+    element (e.g. a framed level buffer) and returns it."""
+    import torch
+    from . import _lib
+    if out is None:
+        out = torch.empty((N, N), dtype=torch.uint8, device=device)
+        ld = N
+        base = out.data_ptr()
+    else:
+        base = out.data_ptr() if isinstance(out, torch.Tensor) else int(out)
+    st = torch.cuda.current_stream(torch.device(device)).cuda_stream
+    rc = _lib.lib().fea_interface_pattern_map(base, int(ld), int(N), int(shape), float(size), st)
+    if rc != 0:
+        raise RuntimeError(f"feanet_amd: fea_interface_pattern_map failed ({rc})")
+    return out

@@ -230,6 +230,39 @@ def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
     return _jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
 
 
+def pbc_pad(u, lo, hi):
+    """Circular extension of the periodic part u[..., :-1, :-1] (period N-1) to (N-1+lo+hi)^2:
+    JacobiBlockPBC.pbc_boundary (FEANet/jacobi.py:72-79) is (1, 2), reset_boundary (:81-84) (0, 1)."""
+    u = _field(u, "u")
+    B, H, W = _bhw(u)
+    if H != W:
+        raise ValueError("feanet_amd: periodic fields are square")
+    M = H - 1 + lo + hi
+    out = torch.empty(u.shape[:-2] + (M, M), dtype=u.dtype, device=u.device)
+    _lib.call("pbc_pad", u.dtype, u.data_ptr(), out.data_ptr(), B, H, lo, hi, _stream(u))
+    return out
+
+
+def jacobi_sweep_pbc(u, f, ktab, omd):
+    """Periodic weighted-Jacobi sweep (JacobiBlockPBC.jacobi_convolution, FEANet/jacobi.py:86-97):
+    u [.., N, N]; f the (N+2)^2 forcing term of the reference's drivers (FNet of the periodic
+    extension); single-pattern stencil ktab; omd = omega/d."""
+    u = _field(u, "u")
+    f = _field(f, "forcing_term", u.dtype)
+    B, H, W = _bhw(u)
+    if H != W or f.shape[-2:] != (H + 2, W + 2) or f.numel() != B * (H + 2) * (W + 2):
+        raise ValueError(f"feanet_amd: periodic sweep needs u [B,1,N,N] and f [B,1,N+2,N+2] "
+                         f"(got {tuple(u.shape)}, {tuple(f.shape)})")
+    tab = _table(ktab, u.dtype, u.device)
+    if tab.shape[0] != 1:
+        raise ValueError("feanet_amd: the periodic sweep is defined for homogeneous meshes (one stencil)")
+    om = torch.as_tensor(omd).to(device=u.device, dtype=u.dtype).reshape(-1)[:1].contiguous()
+    out = torch.empty_like(u)
+    _lib.call("jacobi_sweep_pbc", u.dtype, u.data_ptr(), f.data_ptr(), out.data_ptr(), tab.data_ptr(),
+              om.data_ptr(), B, H, _stream(u))
+    return out
+
+
 def residual(u, f, ktab, pid=None):
     """r = f - K u."""
     if _grad(u, f, ktab):

@@ -29,7 +29,7 @@ from .schedule import OMDF, group_mid, hjac_schedule, vcycle_schedule
 class _Level:
     """Framed buffers of one level: H x W nodes (H = rows, W = columns)."""
 
-    def __init__(self, m, n, B, dtype, device, pid_np=None):
+    def __init__(self, m, n, B, dtype, device, pid_np=None, pid_shape=None):
         self.m, self.n = m, n
         self.H, self.W = m + 1, n + 1
         self.N = self.W
@@ -50,6 +50,11 @@ class _Level:
             p[1:self.H + 1, off:off + self.W] = pid_np
             self.pid = torch.from_numpy(p.reshape(-1)).to(device)
             self.pid = torch.cat([self.pid, torch.zeros(256, dtype=torch.uint8, device=device)])
+        elif pid_shape is not None:  # (shape, size): built on the device straight into the frame
+            off = 128 // esz - 1
+            self.pid = torch.zeros((self.H + 2) * self.ld + 256, dtype=torch.uint8, device=device)
+            ms.interface_pattern_map_device(self.N, pid_shape[0], pid_shape[1], device=device,
+                                            out=self.pid.data_ptr() + self.ld + off, ld=self.ld)
 
     def buf(self, name):
         if name == "zero":
@@ -191,9 +196,9 @@ class MultigridSolver:
         self.levels = []
         for l in range(self.L):
             nl, ml = n >> l, m >> l
-            pid = ms.interface_pattern_map(nl + 1, shape, size) if multi else None
-            self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid))
-        self.fine_pid = (torch.from_numpy(ms.interface_pattern_map(n + 1, shape, size)).to(dev) if multi else None)
+            # two-material pattern maps: built on the device (setup_ops.hip), bit-identical to the host
+            self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid_shape=(shape, size) if multi else None))
+        self.fine_pid = ms.interface_pattern_map_device(n + 1, shape, size, device=dev) if multi else None
         self.tail_from = None
         if coarse_tail:
             esz = 4 if dtype == torch.float32 else 8

@@ -196,6 +196,26 @@ def residual(u, f, pid, ktab):
     return f - knet_apply(u, pid, ktab)
 
 
+def pbc_pad(u, lo, hi):
+    """Circular extension of the periodic part u[..., :-1, :-1] (period n = N-1) by lo rows/columns
+    before and hi after: JacobiBlockPBC.pbc_boundary (FEANet/jacobi.py:72-79) is (lo, hi) = (1, 2),
+    reset_boundary (:81-84) is (0, 1)."""
+    uc = np.asarray(u)[..., :-1, :-1]
+    pad = [(0, 0)] * (uc.ndim - 2) + [(lo, hi), (lo, hi)]
+    return np.pad(uc, pad, mode="wrap")
+
+
+def jacobi_sweep_pbc(u, f, ktab, omega=2. / 3.):
+    """JacobiBlockPBC.jacobi_convolution (FEANet/jacobi.py:86-97), homogeneous mesh: K applied to the
+    (n+3)^2 circular extension with zero padding (KNet.forward, masks padded with 1), cropped to the
+    (n+1)^2 nodes; u_new = omega/d * (f - K u_pbc)[1:-1, 1:-1] + reset_boundary(u).  f is (n+3)^2."""
+    dt = np.asarray(u).dtype.type
+    up = pbc_pad(u, 1, 2)
+    r = (np.asarray(f) - knet_apply(up, np.zeros(up.shape[-2:], np.uint8), ktab))[..., 1:-1, 1:-1]
+    omd = omega_over_d(ktab, omega, dt)[0]
+    return omd * r + pbc_pad(u, 0, 1)
+
+
 def restrict(r, pid, rtab, w0=1.0):
     """Restriction of an (implicitly split) fine field (FEANet/multigrid.py:50-60, 115-122;
     M-FEANet-mg_test.ipynb:27297-27304): crop [1:-1,1:-1], stride-2 3x3 conv with the FINE node's

@@ -531,9 +531,55 @@ def weights():
     print("wrote weights")
 
 
+def pbc_runs():
+    """JacobiBlockPBC (FEANet/jacobi.py:50-97) on MeshSquare grids: circular extension, reset, one and
+    three periodic sweeps, and the residual history of the periodic single-grid driver of
+    Archive/FEA-Net/MM-FEANet/FEANet-periodic.ipynb (cells 2, 5: f = FNet(pbc_boundary(F)),
+    res = ||(f - K pbc_boundary(u))[1:-1, 1:-1]||), in fp32 and fp64."""
+    from FEANet.jacobi import JacobiBlockPBC
+    out = {}
+    for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        torch.set_default_dtype(dt)
+        for n in (8, 16, 32):
+            N = n + 1
+            seed(100 + n)
+            mesh = MeshSquare(2.0, nnode_edge=N)
+            knet = KNet(mesh)
+            fnet = FNet(2.0 / n)
+            if dt == torch.float64:
+                knet, fnet = knet.double(), fnet.double()
+            jac = JacobiBlockPBC(mesh, knet, 2. / 3.)
+            B = 2
+            u = torch.randn(B, 1, N, N, dtype=dt)
+            Fs = torch.randn(B, 1, N, N, dtype=dt)
+            with torch.no_grad():
+                f = fnet(jac.pbc_boundary(Fs))
+                u1 = jac.jacobi_convolution(u, f)
+                u3 = u1
+                for _ in range(2):
+                    u3 = jac.jacobi_convolution(u3, f)
+                v = torch.zeros(1, 1, N, N, dtype=dt)
+                hist = []
+                f0 = f[:1]
+                for _ in range(30):
+                    v = jac.jacobi_convolution(v, f0)
+                    r = f0 - knet(jac.pbc_boundary(v))
+                    hist.append(torch.sqrt(torch.sum(r[:, :, 1:-1, 1:-1] ** 2)).item())
+                out.update({f"{tag}_n{n}_u": t2n(u), f"{tag}_n{n}_F": t2n(Fs), f"{tag}_n{n}_f": t2n(f),
+                            f"{tag}_n{n}_pbc": t2n(jac.pbc_boundary(u)), f"{tag}_n{n}_reset": t2n(jac.reset_boundary(u)),
+                            f"{tag}_n{n}_u1": t2n(u1), f"{tag}_n{n}_u3": t2n(u3), f"{tag}_n{n}_hist": np.array(hist),
+                            f"{tag}_n{n}_v30": t2n(v), f"{tag}_n{n}_dmat": t2n(jac.d_mat)})
+    torch.set_default_dtype(torch.float32)
+    save("pbc_jacobi.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     t0 = time.time()
+    if len(sys.argv) > 1:  # selected generators only, e.g. `make_golden.py pbc_runs`
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     gen_tables()
     gen_ops()
     mg_test_runs()
@@ -545,4 +591,5 @@ if __name__ == "__main__":
     dataset_fixtures()
     recorded_outputs()
     weights()
+    pbc_runs()
     print(f"done in {time.time() - t0:.1f}s")

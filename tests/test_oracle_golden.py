@@ -204,3 +204,27 @@ def test_multigrid_py(gold):
             hist.append(float(mg.residual_norm(v, f)[0]))
         assert len(hist) == len(g[f"{tag}_hist"])
         _hist_close(hist, g[f"{tag}_hist"], 8, 1e-3)
+
+
+@pytest.mark.parametrize("tag", ["f32", "f64"])
+@pytest.mark.parametrize("n", [8, 16, 32])
+def test_oracle_pbc_jacobi(gold, tag, n):
+    """Periodic Jacobi (JacobiBlockPBC, FEANet/jacobi.py:50-97) against the reference's own outputs."""
+    g = gold("pbc_jacobi.npz")
+    ktab, _ = orc.square_mesh(n + 1)
+    u, f = g[f"{tag}_n{n}_u"], g[f"{tag}_n{n}_f"]
+    np.testing.assert_array_equal(orc.pbc_pad(u, 1, 2), g[f"{tag}_n{n}_pbc"])
+    np.testing.assert_array_equal(orc.pbc_pad(u, 0, 1), g[f"{tag}_n{n}_reset"])
+    tol = 1e-5 if tag == "f32" else 1e-13
+    u1 = orc.jacobi_sweep_pbc(u, f, ktab)
+    np.testing.assert_allclose(u1, g[f"{tag}_n{n}_u1"], rtol=0, atol=tol * max(1, np.abs(u1).max()))
+    u3 = orc.jacobi_sweep_pbc(orc.jacobi_sweep_pbc(u1, f, ktab), f, ktab)
+    np.testing.assert_allclose(u3, g[f"{tag}_n{n}_u3"], rtol=0, atol=tol * max(1, np.abs(u3).max()))
+    # the periodic driver's residual history (FEANet-periodic.ipynb cells 2, 5)
+    v = np.zeros_like(u[:1])
+    hist = []
+    for _ in range(30):
+        v = orc.jacobi_sweep_pbc(v, f[:1], ktab)
+        r = f[:1] - orc.knet_apply(orc.pbc_pad(v, 1, 2), np.zeros((n + 3, n + 3), np.uint8), ktab)
+        hist.append(orc.interior_norm(r).sum())
+    np.testing.assert_allclose(hist, g[f"{tag}_n{n}_hist"], rtol=1e-4 if tag == "f32" else 1e-10)

@@ -51,3 +51,25 @@ def test_large_pattern_map_fast():
     pid = ms.interface_pattern_map(2049, 0)
     assert time.time() - t0 < 5.0
     assert pid.shape == (2049, 2049) and pid.max() < 16
+
+
+def test_vtk_export_roundtrip(tmp_path):
+    """MeshCenterInterface(outfile=...) / save_mesh without meshio: legacy binary VTK with the
+    reference's points, quad cells and element phases (FEANet/mesh.py:44-60, 62-68, 119-120)."""
+    from FEANet.mesh import MeshCenterInterface, MeshSquare, read_vtk_legacy
+    from feanet_amd import mesh_setup as ms
+    N = 17
+    p = tmp_path / "plate.vtk"
+    m = MeshCenterInterface(nnode_edge=N, shape=1, outfile=str(p))
+    d = read_vtk_legacy(str(p))
+    np.testing.assert_array_equal(d["points"], m.points)
+    np.testing.assert_array_equal(d["cells"], m.cells)
+    assert (d["types"] == 9).all()
+    np.testing.assert_array_equal(d["CELL_DATA"]["Phase"], ms.element_phase(N, 1).reshape(-1))
+    q = tmp_path / "sq.vtk"
+    sq = MeshSquare(nnode_edge=N)
+    u = np.linspace(0, 1, N * N)
+    sq.save_mesh(str(q), point_data={"u": u})
+    d = read_vtk_legacy(str(q))
+    assert (d["CELL_DATA"]["Phase"] == 0).all()
+    np.testing.assert_array_equal(d["POINT_DATA"]["u"], u)
