@@ -384,7 +384,9 @@ class DDSolver:
 
     # ------------------------------------------------------------------ plan
     def _segs_of(self, steps):
-        """Kernel steps -> [("k", launches) | ("c", comm step)] with consecutive kernels merged."""
+        """Kernel steps -> [("k", launches, touches_level0) | ("c", comm step, False)], consecutive
+        kernels merged; a kernel segment is cut before its first level-0 launch, so the level-0 halo
+        exchange can complete behind the coarse-level segments in front of it (vcycle)."""
         segs = []
         for st in steps:
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
@@ -393,11 +395,12 @@ class DDSolver:
                 if segs and segs[-1][0] == "c" and segs[-1][1][0] == "exchanges":
                     segs[-1][1][1].append(st[1:])
                 else:
-                    segs.append(("c", ("exchanges", [st[1:]])))
+                    segs.append(("c", ("exchanges", [st[1:]]), False))
                 continue
             if st[0] == "gather" and self.P > 1:
-                segs.append(("c", st))
+                segs.append(("c", st, False))
                 continue
+            lvl0 = st[0] == "join" or (st[0] not in ("gather", "scatter", "coarse") and st[1] == 0)
             if st[0] == "gather":  # one rank: the all-gather is a device copy
                 launches = [("copy", (self.gather_target(), self.gather_source()))]
             elif st[0] == "scatter":  # a device copy, captured with the kernels around it
@@ -411,10 +414,10 @@ class DDSolver:
                 launches = [self.local._join_call(st[1], self.local._ptr(1, st[2]))]
             else:
                 launches = [self.local.bind_step(st)]
-            if segs and segs[-1][0] == "k":
+            if segs and segs[-1][0] == "k" and (segs[-1][2] or not lvl0):
                 segs[-1][1].extend(launches)
             else:
-                segs.append(("k", launches))
+                segs.append(("k", launches, lvl0))
         return segs
 
     def joinable(self):
@@ -515,17 +518,35 @@ class DDSolver:
         if self.comm is None:
             raise RuntimeError("DDSolver.vcycle: no communicator (use LocalGroup for in-process ranks)")
         keys, end = self.program(k)
+        pending = None  # level-0 halo exchange in flight (overlaps the coarse levels' kernels)
         for key in keys:
             segs, _ = self.chunk(key)
-            for i, (kind, st) in enumerate(segs):
+            for i, (kind, st, lvl0) in enumerate(segs):
                 if kind == "k":
+                    if lvl0 and pending is not None:
+                        self.comm.exchange_finish(pending)
+                        pending = None
                     self.run_kernels(key, i)
                 elif st[0] == "exchanges":
-                    self.comm.exchange_many(self, st[1])
+                    # coarse-level halos first (the next kernel needs them), the finest iterate's
+                    # halo after, not waited for until a level-0 kernel runs: on RCCL both go out on
+                    # the communicator's stream in this order, so the compute stream only waits for
+                    # the first batch and level 1 .. Ld-1 run while the finest rows are in flight
+                    now = [it for it in st[1] if it[0] != 0]
+                    later = [it for it in st[1] if it[0] == 0]
+                    if pending is not None:
+                        self.comm.exchange_finish(pending)
+                        pending = None
+                    if now:
+                        self.comm.exchange_many(self, now)
+                    if later:
+                        pending = self.comm.exchange_many(self, later, wait=False)
                 elif st[0] == "gather":
                     self.comm.allgather(self.gather_target(), self.gather_source())
                 elif st[0] == "scatter":
                     self.scatter(st[1])
+        if pending is not None:
+            self.comm.exchange_finish(pending)
         self._state = end
 
     def residual_norm(self):
@@ -562,10 +583,12 @@ class TorchComm:
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])
 
-    def exchange_many(self, s, items):
+    def exchange_many(self, s, items, wait=True):
         """Refresh d ghost rows on both sides of rank s's slab for every (level, buffer, d) in `items`,
         as ONE batch of P2P ops.  The op lists are built once per item list and reused (fixed device
-        views)."""
+        views).  wait=False: return a handle for exchange_finish instead of completing the batch (with
+        RCCL the ops run on the communicator's stream meanwhile; finishing makes the current stream
+        wait for them, the host does not block)."""
         dist = self.dist
         key = (id(s), tuple(items))
         plan = self._plans.get(key) if hasattr(self, "_plans") else None
@@ -595,11 +618,21 @@ class TorchComm:
             self._plans[key] = plan
         ops, direct, spairs, rpairs = plan
         if not ops:
-            return
+            return None
         if not direct:
             for b, t in spairs:
                 b.copy_(t)
-        for w in dist.batch_isend_irecv(ops):
+        handle = (dist.batch_isend_irecv(ops), direct, rpairs)
+        if not wait:
+            return handle
+        self.exchange_finish(handle)
+        return None
+
+    def exchange_finish(self, handle):
+        if handle is None:
+            return
+        works, direct, rpairs = handle
+        for w in works:
             w.wait()
         if not direct:
             for b, t in rpairs:
@@ -646,7 +679,7 @@ class LocalGroup:
         keys, end = r0.program(k)
         for key in keys:
             segs, _ = r0.chunk(key)
-            for i, (kind, st) in enumerate(segs):
+            for i, (kind, st, _) in enumerate(segs):
                 if kind == "k":
                     for s in self.ranks:
                         s.chunk(key)
