@@ -36,6 +36,13 @@ struct Frame {
 constexpr int kRB = 32;     // fine rows per task (even: tasks start on odd rows)
 constexpr int kWaves = 4;   // waves (tasks) per block
 constexpr int kTabStride = 10;  // LDS table row: 9 stencil weights + omega/d
+// The restricted field f_c (a quarter of the level's bytes) is stored with normal stores even when
+// the level's own stores stream past the caches: the next kernel (the coarse level's restriction)
+// reads it straight back, from the Infinity Cache instead of HBM.
+#ifndef FEA_COARSE_NT
+#define FEA_COARSE_NT 0
+#endif
+constexpr bool kCoarseNT = FEA_COARSE_NT != 0;
 
 static inline int div_up(int a, int b) { return (a + b - 1) / b; }
 
@@ -536,7 +543,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     }
     T* cp = cb + (long long)(I + 1) * g.ldc;
     if (Jl + Q - 1 <= Wc - 2) {
-      vstore<T, Q, NT>(cp, o);
+      vstore<T, Q, kCoarseNT && NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
     if (!own) return;
     T* cp = cb + (long long)(I + 1) * g.ldc;
     if (J0 + Q - 1 <= Wc - 2) {
-      vstore<T, Q, NT>(cp, o);
+      vstore<T, Q, kCoarseNT && NT>(cp, o);
     } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
@@ -1218,7 +1225,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
               if (own) {
                 T* cp = cb + (long long)(I + 1) * ldc;
                 if (J0 + Q - 1 <= Wc - 2) {
-                  vstore<T, Q, NT>(cp, o);
+                  vstore<T, Q, kCoarseNT && NT>(cp, o);
                 } else {
 #pragma unroll
                   for (int q = 0; q < Q; ++q)
