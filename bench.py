@@ -196,6 +196,11 @@ def dd_domain(P, n0):
 
 
 def main():
+    # stdout carries exactly ONE line, the JSON record: everything else a library writes to fd 1
+    # (RCCL prints its version banner there when the communicator comes up) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -337,7 +342,7 @@ def main():
     elif rank == 0:
         rec["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec), file=json_out, flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
