@@ -385,8 +385,9 @@ class DDSolver:
     # ------------------------------------------------------------------ plan
     def _segs_of(self, steps):
         """Kernel steps -> [("k", launches, touches_level0) | ("c", comm step, False)], consecutive
-        kernels merged; a kernel segment is cut before its first level-0 launch, so the level-0 halo
-        exchange can complete behind the coarse-level segments in front of it (vcycle)."""
+        kernels merged into one segment (one graph launch); segments that touch level 0 are flagged, so
+        the level-0 halo exchange completes only before them (vcycle) — behind the coarse-level
+        segments and the all-gather in front of them."""
         segs = []
         for st in steps:
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
@@ -414,8 +415,10 @@ class DDSolver:
                 launches = [self.local._join_call(st[1], self.local._ptr(1, st[2]))]
             else:
                 launches = [self.local.bind_step(st)]
-            if segs and segs[-1][0] == "k" and (segs[-1][2] or not lvl0):
+            if segs and segs[-1][0] == "k":
                 segs[-1][1].extend(launches)
+                if lvl0:
+                    segs[-1] = ("k", segs[-1][1], True)
             else:
                 segs.append(("k", launches, lvl0))
         return segs
