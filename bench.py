@@ -125,29 +125,43 @@ def time_fine_kernels(s, reps):
 
 
 def time_join_in_cycle(s, k):
-    """The cycle-join kernel timed INSIDE the V-cycle: vcycle(k)'s launch sequence replayed eagerly on
-    the solver's stream (same kernels, same buffers, same cache history as the graph replays), with
-    HIP events recorded on that stream around every fea_mg_cycle_join launch.  Returns the average
-    seconds per join launch (None if the solver does not join cycles)."""
+    """The cycle-join kernel timed INSIDE the V-cycle with HIP events on the solver's stream: two eager
+    replays of vcycle(k)'s launch sequence (same kernels, buffers and cache history as the graph
+    replays); in the first an event pair brackets [the launch before each join, the join], in the
+    second [the launch before each join] alone.  The difference of the two averages is the join's
+    duration with the event pair's own dispatch overhead cancelled.  Returns seconds per join
+    (None if the solver does not join cycles)."""
     from feanet_amd import _lib
     if not s._joinable() or k < 2:
         return None
     st = torch.cuda.current_stream()
-    prog, end = s.joined_program(k)
-    ev = []
-    for _, launches in prog:
-        for name, args in launches:
-            if name == "mg_cycle_join":
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st)
-                _lib.call(name, s.dtype, *args, st.cuda_stream)
-                e1.record(st)
-                ev.append((e0, e1))
-            else:
-                _lib.call(name, s.dtype, *args, st.cuda_stream)
-    s._state = end
-    ev[-1][1].synchronize()
-    return sum(a.elapsed_time(b) for a, b in ev) / len(ev) * 1e-3
+
+    def replay(with_join):
+        prog, end = s.joined_program(k)
+        ev = []
+        for _, launches in prog:
+            for i, (name, args) in enumerate(launches):
+                nxt = launches[i + 1][0] if i + 1 < len(launches) else None
+                if nxt == "mg_cycle_join":  # the launch before a join opens the bracket
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    _lib.call(name, s.dtype, *args, st.cuda_stream)
+                    if not with_join:
+                        e1.record(st)
+                    ev.append((e0, e1))
+                elif name == "mg_cycle_join":
+                    _lib.call(name, s.dtype, *args, st.cuda_stream)
+                    if with_join:
+                        ev[-1][1].record(st)
+                else:
+                    _lib.call(name, s.dtype, *args, st.cuda_stream)
+        s._state = end
+        ev[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev) * 1e-3
+
+    with_join = replay(True)
+    without = replay(False)
+    return with_join - without
 
 
 def load_traffic(kernel_key):
@@ -292,7 +306,8 @@ def main():
     # roofline: the DOMINANT kernel of the timed region — the finest level's cycle join (one per V-cycle
     # boundary, ~45 % of the V-cycle), timed inside the cycle with HIP events on the solver's stream
     jt = time_join_in_cycle(s, min(args.steps, 200)) if mode == "single" else None
-    jsrc = "HIP events around every fea_mg_cycle_join launch of an eager replay of vcycle(K), in its stream"
+    jsrc = ("HIP events in the solver's stream, eager replays of vcycle(K): [previous launch + join] minus "
+            "[previous launch] per cycle")
     if jt is None and "fea_mg_cycle_join" in fine:
         jt = fine["fea_mg_cycle_join"][0]
         jsrc = "HIP events, back-to-back launches of fea_mg_cycle_join on the level-0 buffers"
