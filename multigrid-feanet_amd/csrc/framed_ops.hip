@@ -492,24 +492,33 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   WRow W0 = fin_w(raw_w(y0 - 1), y0 - 1);
   WRow W1 = fin_w(raw_w(y0), y0);
   WRow W2 = fin_w(raw_w(y0 + 1), y0 + 1);
-  RawW n1 = raw_w(2 * I0 + 1), n2 = raw_w(2 * I0 + 2);
+  // the fine rows of the next TWO coarse rows are in flight, in a two-slot ring indexed by the
+  // iteration's parity (compile-time after the unroll below): a slot is consumed in place and
+  // refilled at once, so no in-flight register is ever copied (a copy waits for its load)
+  RawW ring[2][2];
+  ring[0][0] = raw_w(2 * I0 + 1);
+  ring[0][1] = raw_w(2 * I0 + 2);
+  ring[1][0] = raw_w(2 * I0 + 3);
+  ring[1][1] = raw_w(2 * I0 + 4);
   T Ra[V + 1], Rb[V + 1], Rc[V + 1];
   PRow<V> Pa = W1.p, Pb, Pc;
   resid(W0, W1, W2, Ra);
   store_v(y0, W1);
-  for (int I = I0; I < I1; ++I) {
-    const RawW m1 = raw_w(2 * I + 3), m2 = raw_w(2 * I + 4);  // next coarse row's fine rows
+  auto iter = [&](int I, auto slot) {
+    constexpr int S = decltype(slot)::value;
     // fine row 2I
     W0 = W1;
     W1 = W2;
-    W2 = fin_w(n1, 2 * I + 1);
+    W2 = fin_w(ring[S][0], 2 * I + 1);
+    ring[S][0] = raw_w(2 * I + 5);
     resid(W0, W1, W2, Rb);
     Pb = W1.p;
     store_v(2 * I, W1);
     // fine row 2I+1
     W0 = W1;
     W1 = W2;
-    W2 = fin_w(n2, 2 * I + 2);
+    W2 = fin_w(ring[S][1], 2 * I + 2);
+    ring[S][1] = raw_w(2 * I + 6);
     resid(W0, W1, W2, Rc);
     Pc = W1.p;
     store_v(2 * I + 1, W1);
@@ -552,9 +561,13 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
     Pa = Pc;
-    n1 = m1;
-    n2 = m2;
+  };
+  int I = I0;
+  for (; I + 1 < I1; I += 2) {
+    iter(I, std::integral_constant<int, 0>{});
+    iter(I + 1, std::integral_constant<int, 1>{});
   }
+  if (I < I1) iter(I, std::integral_constant<int, 0>{});
 }
 
 // ---------------------------------------------------------------------------
