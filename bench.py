@@ -104,23 +104,24 @@ def time_fine_kernels(s, reps):
     cnodes = L1.B * (L1.H - 2) * (L1.W - 2)
     geom = L0.geom()
     kt, om, nt = s.ktab.data_ptr(), s.omd.data_ptr(), s.ntab
+    p0 = None if L0.pid is None else L0.pid.data_ptr()
+    p1 = None if L1.pid is None else L1.pid.data_ptr()
+    nr, npt = s.rtab.shape[0], s.ptab.shape[0]
+    pb = 1 if L0.pid is not None else 0  # two-material problems read a pattern byte per node
     out = {}
-    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, kt, om, nt) + geom
-    out["fea_mg_sweep"] = (time_kernel("mg_sweep", s.dtype, args, reps, st), 3 * es * nodes)
-    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), L1.f.data_ptr(), None, kt, om, nt,
-            s.rtab.data_ptr(), s.rtab.shape[0], s.w[0]) + geom + (L1.ld, L1.bs)
+    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), p0, kt, om, nt) + geom
+    out["fea_mg_sweep"] = (time_kernel("mg_sweep", s.dtype, args, reps, st), (3 * es + pb) * nodes)
+    args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), L1.f.data_ptr(), p0, kt, om, nt,
+            s.rtab.data_ptr(), nr, s.w[0]) + geom + (L1.ld, L1.bs)
     out["fea_mg_sweep_restrict"] = (time_kernel("mg_sweep_restrict", s.dtype, args, reps, st),
-                                    3 * es * nodes + es * cnodes)
-    args = (L0.a.data_ptr(), L1.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), None, None, kt, om, nt,
-            s.ptab.data_ptr(), s.ptab.shape[0], s.w[1]) + geom + (L1.ld, L1.bs)
+                                    (3 * es + pb) * nodes + es * cnodes)
+    args = (L0.a.data_ptr(), L1.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), p0, p1, kt, om, nt,
+            s.ptab.data_ptr(), npt, s.w[1]) + geom + (L1.ld, L1.bs)
     out["fea_mg_prolong_sweep"] = (time_kernel("mg_prolong_sweep", s.dtype, args, reps, st),
-                                   3 * es * nodes + es * cnodes)
-    if L0.pid is None:
-        args = (L0.a.data_ptr(), L1.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), L1.f.data_ptr(), None, None, kt,
-                om, nt, s.ptab.data_ptr(), s.ptab.shape[0], s.rtab.data_ptr(), s.rtab.shape[0], s.w[1],
-                s.w[0]) + geom + (L1.ld, L1.bs)
-        out["fea_mg_cycle_join"] = (time_kernel("mg_cycle_join", s.dtype, args, reps, st),
-                                    3 * es * nodes + 2 * es * cnodes)
+                                   (3 * es + pb) * nodes + (es + pb) * cnodes)
+    name, args = s._join_call("a", L1.a.data_ptr())
+    out["fea_mg_cycle_join"] = (time_kernel(name, s.dtype, args, reps, st),
+                                (3 * es + pb) * nodes + (2 * es + pb) * cnodes)
     return out
 
 
