@@ -1,0 +1,145 @@
+"""The generic HIP operators as PyTorch custom ops: `torch.ops.feanet.<name>`.
+
+BASELINE.json's north star asks for the kernels to be "surfaced to the Python host as PyTorch-ROCm
+custom ops".  Each op below is registered with torch.library for the HIP ('cuda') device only; its
+implementation is the ctypes call of feanet_amd.ops (one HIP kernel, the caller's current stream), a
+fake implementation gives output shapes for tracing / meta tensors, and knet_apply / residual carry
+their HIP adjoints (feanet_amd.autograd) through register_autograd.  CPU tensors find no kernel and
+raise — there is no CPU fallback.  The FEANet modules call feanet_amd.ops directly (same kernels).
+
+  feanet::knet_apply(u, ktab, pid?)                   KNet.forward        FEANet/model.py:22-30
+  feanet::residual(u, f, ktab, pid?)                  f - K u             FEANet/multigrid.py:168
+  feanet::jacobi_sweep(u, f, ktab, omd, pid?, geo?, bc?)  jacobi_convolution  FEANet/jacobi.py:39-47
+  feanet::restrict(x, rtab, w0, pid?)                 MultiGrid.Restrict  FEANet/multigrid.py:115-122
+  feanet::prolong(e, ptab, w1, pidc?, add?)           MultiGrid.Interpolate FEANet/multigrid.py:124-130
+  feanet::residual_norm(u, f?, ktab?, pid?)           driver residual norm M-FEANet-mg_test.ipynb:27428
+  feanet::pbc_pad(u, lo, hi)                          JacobiBlockPBC.pbc_boundary / reset_boundary
+  feanet::jacobi_sweep_pbc(u, f, ktab, omd)           JacobiBlockPBC.jacobi_convolution FEANet/jacobi.py:86-97
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import autograd as _ag
+from . import ops
+
+_DEV = "cuda"
+
+
+@torch.library.custom_op("feanet::knet_apply", mutates_args=(), device_types=_DEV)
+def knet_apply(u: Tensor, ktab: Tensor, pid: Optional[Tensor] = None) -> Tensor:
+    return ops._knet_apply(u, ktab, pid)
+
+
+@knet_apply.register_fake
+def _(u, ktab, pid=None):
+    return torch.empty_like(u, memory_format=torch.contiguous_format)
+
+
+def _knet_setup(ctx, inputs, output):
+    u, ktab, pid = inputs
+    ctx.save_for_backward(u, ktab, pid)
+
+
+def _knet_bwd(ctx, g):
+    u, ktab, pid = ctx.saved_tensors
+    gu = _ag._knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
+    gk = _ag._stencil_grad(g, u, ktab, pid) if ctx.needs_input_grad[1] else None
+    return gu, gk, None
+
+
+knet_apply.register_autograd(_knet_bwd, setup_context=_knet_setup)
+
+
+@torch.library.custom_op("feanet::residual", mutates_args=(), device_types=_DEV)
+def residual(u: Tensor, f: Tensor, ktab: Tensor, pid: Optional[Tensor] = None) -> Tensor:
+    return ops._residual(u, f, ktab, pid)
+
+
+@residual.register_fake
+def _(u, f, ktab, pid=None):
+    return torch.empty_like(u, memory_format=torch.contiguous_format)
+
+
+def _res_setup(ctx, inputs, output):
+    u, f, ktab, pid = inputs
+    ctx.save_for_backward(u, ktab, pid)
+
+
+def _res_bwd(ctx, g):
+    u, ktab, pid = ctx.saved_tensors
+    gu = -_ag._knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
+    gf = g if ctx.needs_input_grad[1] else None
+    gk = _ag._stencil_grad(g, u, ktab, pid, -1.0) if ctx.needs_input_grad[2] else None
+    return gu, gf, gk, None
+
+
+residual.register_autograd(_res_bwd, setup_context=_res_setup)
+
+
+@torch.library.custom_op("feanet::jacobi_sweep", mutates_args=(), device_types=_DEV)
+def jacobi_sweep(u: Tensor, f: Tensor, ktab: Tensor, omd: Tensor, pid: Optional[Tensor] = None,
+                 geo: Optional[Tensor] = None, bc: Optional[Tensor] = None) -> Tensor:
+    return ops._jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
+
+
+@jacobi_sweep.register_fake
+def _(u, f, ktab, omd, pid=None, geo=None, bc=None):
+    return torch.empty_like(u, memory_format=torch.contiguous_format)
+
+
+@torch.library.custom_op("feanet::restrict", mutates_args=(), device_types=_DEV)
+def restrict(x: Tensor, rtab: Tensor, w0: float = 1.0, pid: Optional[Tensor] = None) -> Tensor:
+    return ops._restrict(x, rtab, w0, pid)
+
+
+@restrict.register_fake
+def _(x, rtab, w0=1.0, pid=None):
+    B, _, H, W = x.shape
+    return x.new_empty((B, 1, (H + 1) // 2, (W + 1) // 2))
+
+
+@torch.library.custom_op("feanet::prolong", mutates_args=(), device_types=_DEV)
+def prolong(e: Tensor, ptab: Tensor, w1: float = 1.0, pidc: Optional[Tensor] = None,
+            add: Optional[Tensor] = None) -> Tensor:
+    return ops._prolong(e, ptab, w1, pidc, add)
+
+
+@prolong.register_fake
+def _(e, ptab, w1=1.0, pidc=None, add=None):
+    B, _, Hc, Wc = e.shape
+    return e.new_empty((B, 1, 2 * Hc - 1, 2 * Wc - 1))
+
+
+@torch.library.custom_op("feanet::residual_norm", mutates_args=(), device_types=_DEV)
+def residual_norm(u: Tensor, f: Optional[Tensor] = None, ktab: Optional[Tensor] = None,
+                  pid: Optional[Tensor] = None) -> Tensor:
+    return ops.residual_norm(u, f, ktab, pid)
+
+
+@residual_norm.register_fake
+def _(u, f=None, ktab=None, pid=None):
+    H, W = u.shape[-2:]
+    return u.new_empty((u.numel() // (H * W),), dtype=torch.float64)
+
+
+@torch.library.custom_op("feanet::pbc_pad", mutates_args=(), device_types=_DEV)
+def pbc_pad(u: Tensor, lo: int, hi: int) -> Tensor:
+    return ops.pbc_pad(u, lo, hi)
+
+
+@pbc_pad.register_fake
+def _(u, lo, hi):
+    M = u.shape[-1] - 1 + lo + hi
+    return u.new_empty(u.shape[:-2] + (M, M))
+
+
+@torch.library.custom_op("feanet::jacobi_sweep_pbc", mutates_args=(), device_types=_DEV)
+def jacobi_sweep_pbc(u: Tensor, f: Tensor, ktab: Tensor, omd: Tensor) -> Tensor:
+    return ops.jacobi_sweep_pbc(u, f, ktab, omd)
+
+
+@jacobi_sweep_pbc.register_fake
+def _(u, f, ktab, omd):
+    return torch.empty_like(u, memory_format=torch.contiguous_format)
