@@ -76,12 +76,17 @@ struct VecOf<float, 4> { typedef float type __attribute__((ext_vector_type(4)));
 template <>
 struct VecOf<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
 
-template <typename T, int V>
+template <typename T, int V, bool NTL = false>
 __device__ __forceinline__ void vload(const T* p, T (&x)[V]) {
   if constexpr (V == 1) {
     x[0] = *p;
   } else {
-    const typename VecOf<T, V>::type v = *reinterpret_cast<const typename VecOf<T, V>::type*>(p);
+    const auto* q = reinterpret_cast<const typename VecOf<T, V>::type*>(p);
+    typename VecOf<T, V>::type v;
+    if constexpr (NTL)
+      v = __builtin_nontemporal_load(q);
+    else
+      v = *q;
 #pragma unroll
     for (int k = 0; k < V; ++k) x[k] = v[k];
   }
@@ -1035,6 +1040,11 @@ __device__ __forceinline__ X& pick(X& a, X& b) {
 #define FEA_JOIN_WAVES 0
 #endif
 static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of 2 or 4 rows");
+// FEA_JOIN_NTL: nontemporal loads of the iterate u in the join on levels above the NT threshold
+#ifndef FEA_JOIN_NTL
+#define FEA_JOIN_NTL 1
+#endif
+constexpr bool kJoinNTL = FEA_JOIN_NTL != 0;
 
 template <typename T>
 struct Ovl3 {
@@ -1126,7 +1136,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
   int pb_[kJoinAhead][V];
 #pragma unroll
   for (int q = 0; q < kJoinAhead; ++q) {
-    vload<T, V>(ub + rowo(ys + q), ub_[q]);
+    vload<T, V, kJoinNTL && NT>(ub + rowo(ys + q), ub_[q]);
     vload<T, V>(fb + rowo(ys + q - 1), fb_[q]);
     if constexpr (MULTI) pload<V>(pb + rowo(ys + q), pb_[q]);
   }
@@ -1162,7 +1172,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
       fy1[k] = bf[k];
       if constexpr (MULTI) p0[k] = bp[k];
     }
-    vload<T, V>(ub + rowo(y + kJoinAhead), bu);
+    vload<T, V, kJoinNTL && NT>(ub + rowo(y + kJoinAhead), bu);
     vload<T, V>(fb + rowo(y + kJoinAhead - 1), bf);
     if constexpr (MULTI) pload<V>(pb + rowo(y + kJoinAhead), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
