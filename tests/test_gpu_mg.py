@@ -559,6 +559,24 @@ def test_cycle_join_bitwise(T, problem, n, m, B, k):
     assert torch.equal(out[0][1], out[1][1])
 
 
+def test_cycle_join_bitwise_full_size():
+    """At 4097^2 fp64 the finest fields exceed the nontemporal threshold (64 MiB): the join then streams
+    u with nontemporal loads and stores u' nontemporally; still bitwise the unjoined cycles."""
+    from feanet_amd.solver import MultigridSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    f = torch.randn(1, 1, 4097, 4097, device="cuda", dtype=torch.float64, generator=g)
+    out = []
+    for join in (False, True):
+        s = MultigridSolver(4096, dtype=torch.float64, join_cycles=join)
+        s.set_rhs(f=f)
+        s.load()
+        s.vcycle(3)
+        out.append(s.solution())
+        del s
+    assert torch.equal(out[0], out[1])
+
+
 def test_cycle_join_kernel_direct():
     """fea_mg_cycle_join against fea_mg_prolong_sweep + fea_mg_sweep_restrict on random data, including
     boundary nodes that are not zero (Dirichlet data) and a coarse correction with a nonzero ring."""
