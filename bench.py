@@ -177,28 +177,58 @@ def load_traffic(kernel_key):
         return None, None
 
 
-def cpu_baseline(n, seconds_budget=20.0):
-    """Oracle (numpy, single thread) V-cycles on the same 4097^2 fp64 Poisson workload."""
-    from oracle import feanet_oracle as orc
-    rng = np.random.default_rng(0)
-    N = n + 1
-    f = rng.standard_normal((1, N, N))
-    mg = orc.OracleMultigrid(n, "poisson", np.float64)
-    v = np.zeros((1, N, N))
+def host_threads():
+    """Host cores for the CPU baseline: the process's CPU affinity, capped by OMP_NUM_THREADS
+    when the environment sets it (the GPU box gives one GPU's job a 16-core share of a larger host)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, len(os.sched_getaffinity(0))
+
+
+def _time_cycles(step, v, seconds_budget, max_timed=5):
     t0 = time.perf_counter()
-    v = mg.step(v, f)  # warm-up cycle (page-in, allocation)
-    t1 = time.perf_counter()
-    first = t1 - t0
-    k = max(1, min(5, int(seconds_budget / max(first, 1e-3)) - 1))
+    v = step(v)  # warm-up cycle (page-in, allocation)
+    first = time.perf_counter() - t0
+    k = max(3, min(max_timed, int(seconds_budget / max(first, 1e-3)) - 1))
     times = []
     for _ in range(k):
         t0 = time.perf_counter()
-        v = mg.step(v, f)
+        v = step(v)
         times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    return {"value": N * N / t, "unit": "DoF-updates/s", "cores": 1, "kind": "port",
+    return float(np.median(times)), k
+
+
+def cpu_baseline(n, seconds_budget=16.0):
+    """The reference's PyTorch-CPU formulation (oracle/torch_cpu.py: conv2d identity split + stencil,
+    f - K u, omega/d, stride-2 conv restriction, conv_transpose2d prolongation — MultiGrid.Step of
+    M-FEANet-mg_test.ipynb) on the same 4097^2 fp64 Poisson workload, all host cores of this job; the
+    numpy oracle (1 thread) beside it as a secondary number."""
+    from oracle import feanet_oracle as orc
+    from oracle.torch_cpu import TorchCPUMultigrid
+    threads, affinity = host_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    N = n + 1
+    f = rng.standard_normal((1, 1, N, N))
+    ft = torch.from_numpy(f)
+    mt = TorchCPUMultigrid(n, dtype=torch.float64)
+    with torch.no_grad():
+        t, k = _time_cycles(lambda v: mt.step(v, ft), torch.zeros(1, 1, N, N, dtype=torch.float64), seconds_budget)
+    torch.set_num_threads(prev)
+    mo = orc.OracleMultigrid(n, "poisson", np.float64)
+    tn, kn = _time_cycles(lambda v: mo.step(v, f[:, 0]), np.zeros((1, N, N)), 6.0, max_timed=3)
+    return {"value": N * N / t, "unit": "DoF-updates/s", "cores": threads, "kind": "port",
             "sample": f"{k} timed V-cycles (median {t:.2f} s, +1 warm-up) of the {N}x{N} fp64 Poisson V(1,1) "
-                      f"workload by the numpy oracle (oracle/feanet_oracle.py), 1 thread, host of the GPU box"}
+                      f"workload by the reference's PyTorch-CPU formulation restated op for op "
+                      f"(oracle/torch_cpu.py: conv2d/conv_transpose2d, MultiGrid.Step), torch.set_num_threads({threads}) "
+                      f"(process affinity {affinity} CPUs, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}), "
+                      f"host of the GPU box",
+            "torch_threads": threads,
+            "numpy_oracle_1thread": {"value": N * N / tn, "unit": "DoF-updates/s", "cores": 1,
+                                     "sample": f"{kn} V-cycles (median {tn:.2f} s) by oracle/feanet_oracle.py"}}
 
 
 def dd_domain(P, n0):
@@ -274,17 +304,16 @@ def main():
     conv = float((s.residual_norm().max() / r0.max()).item()) ** (1.0 / 8)
     s.load()
 
-    # warm-up: two multi-cycle calls, so every launch segment of the timed call (first cycle, joined
-    # cycle boundaries in both buffer parities, last cycle) has run once eagerly and been captured
-    # warm-up: multi-cycle calls covering both buffer parities, so every launch segment the timed call
-    # replays (first cycle, graphs of GRAPH_CYCLES joined cycles, single joined cycles, last cycle) has
-    # run once eagerly and been captured before the clock starts
-    G = getattr(s, "GRAPH_CYCLES", 0) if mode == "single" else 0
-    wk = max(3, args.warmup, 2 * G + 2)
+    # warm-up: the timed call itself (vcycle(steps)), repeated so that it has started from both
+    # ping-pong buffers at least twice: every graph the timed call replays (its blocks of joined
+    # cycles, keyed by start buffer and size) has run once eagerly and been captured before the clock
+    # starts.  At least --warmup cycles in total.
+    calls = max(4, -(-args.warmup // args.steps))
+    calls += calls % 2
     warm = 0
-    for extra in (0, 1, 0, 1):
-        s.vcycle(wk + extra)
-        warm += wk + extra
+    for _ in range(calls):
+        s.vcycle(args.steps)
+        warm += args.steps
     torch.cuda.synchronize()
     barrier(ws)
     torch.cuda.synchronize()

@@ -593,11 +593,12 @@ class TorchComm:
         RCCL the ops run on the communicator's stream meanwhile; finishing makes the current stream
         wait for them, the host does not block)."""
         dist = self.dist
-        key = (id(s), tuple(items))
-        plan = self._plans.get(key) if hasattr(self, "_plans") else None
+        # plans hold views of s's buffers: cached on s itself (keyed by this communicator), never on
+        # the communicator under id(s), which a later solver could reuse
+        plans = s.__dict__.setdefault("_comm_plans", {})
+        key = (id(self), tuple(items))
+        plan = plans.get(key)
         if plan is None:
-            if not hasattr(self, "_plans"):
-                self._plans = {}
             sends, recvs = [], []
             for l, name, d in items:
                 lp = s.parts[l]
@@ -618,7 +619,7 @@ class TorchComm:
             ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, (_, peer) in zip(sb, sends)]
             ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, (_, peer) in zip(rb, recvs)]
             plan = (ops, direct, list(zip(sb, [t for t, _ in sends])), list(zip(rb, [t for t, _ in recvs])))
-            self._plans[key] = plan
+            plans[key] = plan
         ops, direct, spairs, rpairs = plan
         if not ops:
             return None

@@ -501,26 +501,42 @@ class MultigridSolver:
         prog.append((("tail", pre), mid + [tail]))
         return prog, other(pre)
 
-    GRAPH_CYCLES = int(os.environ.get("FEANET_GRAPH_CYCLES", "32"))  # joined cycles per HIP graph
+    GRAPH_CYCLES = int(os.environ.get("FEANET_GRAPH_CYCLES", "32"))  # max joined cycles per HIP graph
+
+    @staticmethod
+    def graph_blocks(njoin, G):
+        """Block sizes the njoin cycle joins of vcycle(njoin + 1) are replayed in: as many blocks of G
+        (a power of two) as fit, then the binary decomposition of the remainder, largest first."""
+        blocks = [G] * (njoin // G)
+        r = njoin % G
+        b = G
+        while r:
+            b //= 2
+            if r >= b:
+                blocks.append(b)
+                r -= b
+        return blocks
 
     def _vcycles_joined(self, k):
-        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles).
-        Runs of GRAPH_CYCLES joined cycles are captured as ONE graph (an even count, so a run starts
-        and ends in the same buffer and the graph replays for every run): each graph launch costs
-        ~8 us of dispatch gap on the GPU, paid once per run instead of once per cycle."""
+        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles),
+        replayed as FEW HIP graphs whatever k is: the k - 1 joined cycles go in blocks of GRAPH_CYCLES
+        plus the binary decomposition of the remainder (graph_blocks); the first block also carries the
+        first cycle's head, the last block the last cycle's tail.  Each graph launch costs ~8 us of
+        dispatch gap on the GPU, so vcycle(20) pays it 3 times (16 + 2 + 1), vcycle(1000) 34 times.
+        A block's graph is keyed by (start buffer, size, head?, tail?): at most 2 x 2 x 2 x log2(G)+1
+        graphs, each captured on its second use."""
         prog, end = self.joined_program(k)
-        G = self.GRAPH_CYCLES - self.GRAPH_CYCLES % 2
+        G = max(1, self.GRAPH_CYCLES)
+        G = 1 << (G.bit_length() - 1)
+        head, joins, tail = prog[0], prog[1:-1], prog[-1]
+        blocks = self.graph_blocks(len(joins), G)
         i = 0
-        while i < len(prog):
-            key, launches = prog[i]
-            if G >= 2 and key[0] == "join" and i + G <= len(prog) and all(
-                    prog[j][0][0] == "join" for j in range(i, i + G)):
-                block = [ln for _, seg in prog[i:i + G] for ln in seg]
-                self._run_segment(("joinblock", key[1], G), block)
-                i += G
-                continue
-            self._run_segment(key, launches)
-            i += 1
+        for bi, nb in enumerate(blocks):
+            first, last = bi == 0, bi == len(blocks) - 1
+            segs = ([head] if first else []) + joins[i:i + nb] + ([tail] if last else [])
+            key = ("block", joins[i][0][1], nb, first, last)
+            self._run_segment(key, [ln for _, seg in segs for ln in seg])
+            i += nb
         self._state = end
 
     def vcycle(self, k=1):

@@ -40,7 +40,6 @@ def test_c2_1025_six_levels_vs_oracle():
 
 
 def test_c3_2049_interface_learned_ratio():
-    from feanet_amd import mesh_setup as ms
     from feanet_amd.solver import MultigridSolver
     w = np.load(os.path.join(HERE, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
     n = 2048
@@ -51,15 +50,16 @@ def test_c3_2049_interface_learned_ratio():
     r0 = float(s.residual_norm()[0])
     s.vcycle()
     got = s.solution().cpu().numpy()[:, 0]
-    # oracle: same operators; pattern maps from the vectorised builder (bit-exact with the reference's
-    # loop at every size the reference can build, tests/test_setup.py)
+    # oracle: same operators; pattern maps computed by the ORACLE's own element/node loop
+    # (tests/golden/c3_pattern_maps.npz, made by tests/golden/make_c3_maps.py and re-checked against
+    # the loop in the CPU suite, tests/test_setup.py::test_c3_maps_fixture_is_oracle)
+    maps = np.load(os.path.join(HERE, "golden", "c3_pattern_maps.npz"))
     mg = orc.OracleMultigrid(256, "poisson", np.float64)  # placeholder hierarchy, levels replaced below
     mg.levels = []
-    ktab = ms.stencil_table((1, 20))
     for l in range(s.L):
         lv = orc.Level(n >> l, "poisson", np.float64)
-        lv.ktab = ktab
-        lv.pid = ms.interface_pattern_map((n >> l) + 1)
+        lv.ktab = maps["ktab"]
+        lv.pid = maps[f"pid_{(n >> l) + 1}"]
         mg.levels.append(lv)
     mg.L = s.L
     mg.rtab = np.broadcast_to(np.asarray(w["R"][0], np.float32), (16, 3, 3))

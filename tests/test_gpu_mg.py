@@ -81,10 +81,20 @@ def rand_state(rng, B, N, T, bc_scale=1.0):
 SIZES = [(2, 1), (4, 3), (8, 1), (16, 3), (128, 1), (256, 3), (1024, 1)]
 
 
+@pytest.fixture(params=[False, True], ids=["cached", "nt"])
+def nt(request, monkeypatch):
+    """nt: FEANET_NT_BYTES=0 forces the nontemporal instantiations of the level kernels (stores past the
+    caches; the cycle join's nontemporal iterate loads) that otherwise only run on levels > 64 MiB, i.e.
+    only at sizes too large for the oracle (the 4097^2 metric configuration)."""
+    if request.param:
+        monkeypatch.setenv("FEANET_NT_BYTES", "0")
+    return request.param
+
+
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
 @pytest.mark.parametrize("n,B", SIZES)
-def test_mg_sweep(T, problem, n, B):
+def test_mg_sweep(T, problem, n, B, nt):
     from feanet_amd import _lib
     if problem == "interface" and n > 256:
         pytest.skip("oracle pattern search kept small")
@@ -122,7 +132,7 @@ def test_mg_sweep(T, problem, n, B):
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem,learned", [("poisson", False), ("interface", False), ("interface", True)])
 @pytest.mark.parametrize("n,B", SIZES[1:])
-def test_mg_transfer(T, problem, learned, n, B):
+def test_mg_transfer(T, problem, learned, n, B, nt):
     from feanet_amd import _lib
     if problem == "interface" and n > 256:
         pytest.skip("oracle pattern search kept small")
@@ -205,7 +215,7 @@ def test_mg_transfer(T, problem, learned, n, B):
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem", ["poisson", "interface"])
 @pytest.mark.parametrize("n,L", [(64, None), (128, 4), (32, 1), (32, 2), (256, None), (1024, None)])
-def test_vcycle_vs_oracle(T, problem, n, L, tail, fuse):
+def test_vcycle_vs_oracle(T, problem, n, L, tail, fuse, nt):
     if problem == "interface" and n > 256:
         pytest.skip("oracle pattern search kept small")
     from feanet_amd.solver import MultigridSolver
@@ -239,6 +249,75 @@ def test_vcycle_vs_oracle(T, problem, n, L, tail, fuse):
         ref = orc.interior_norm(f - mg_o.levels[0].K(v))
         tol = 1e-9 if T == torch.float64 else 2e-3
         np.testing.assert_allclose(res, ref, rtol=tol, atol=(1e-12 if T == torch.float64 else 1e-6) * r0.max())
+
+
+@pytest.mark.parametrize("T", [torch.float64, torch.float32])
+@pytest.mark.parametrize("problem,n,B", [("poisson", 64, 2), ("poisson", 256, 1), ("poisson", 1024, 1),
+                                         ("interface", 128, 2), ("interface", 256, 1)])
+def test_joined_vcycles_vs_oracle(T, problem, n, B, nt):
+    """vcycle(k) with joined cycle boundaries (fea_mg_cycle_join on the finest level, graph-replayed
+    blocks) against k oracle MultiGrid.Step cycles, with random Dirichlet data; cached and
+    nontemporal kernel instantiations.  fp64 to 1e-10 of max|u|; fp32 to 2e-5 after one joined pair."""
+    from feanet_amd.solver import MultigridSolver
+    rng = np.random.default_rng(7 * n + B)
+    N = n + 1
+    mg_o = orc.OracleMultigrid(n, problem, npdt(T))
+    geo, _ = orc.square_geometry(N, npdt(T))
+    bc = (rng.random((B, N, N)) * (1 - geo)).astype(npdt(T))
+    mg_o.set_boundary(geo, bc)
+    u0 = rng.standard_normal((B, N, N)).astype(npdt(T))
+    f = rng.standard_normal((B, N, N)).astype(npdt(T))
+    s = MultigridSolver(n, problem=problem, dtype=T, batch=B)
+    s.set_boundary(torch.from_numpy(bc).cuda().reshape(B, 1, N, N))
+    s.set_rhs(f=torch.from_numpy(f).cuda().reshape(B, 1, N, N))
+    v = u0 * geo + bc
+    for k in ((2, 3) if T == torch.float64 else (2,)):
+        s.load(torch.from_numpy(u0).cuda().reshape(B, 1, N, N))
+        s.vcycle(k)
+        ref = v
+        for _ in range(k):
+            ref = mg_o.step(ref, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        err = np.abs(got - ref).max() / max(1.0, np.abs(ref).max())
+        assert err < (1e-10 if T == torch.float64 else 2e-5), f"k={k}: {err:.3e}"
+
+
+def test_full_size_vs_oracle():
+    """The metric configuration itself: 4097^2 fp64 Poisson, seeded rhs and random Dirichlet data,
+    one V-cycle (fea_mg_sweep_restrict / prolongation kernels) and then three joined V-cycles
+    (fea_mg_cycle_join, nontemporal loads and stores: every level-0 field is > 64 MiB) against the
+    oracle's MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372), 1e-10 of max|u| (~1.5 s per oracle
+    cycle on the host)."""
+    from feanet_amd.solver import MultigridSolver
+    n = 4096
+    N = n + 1
+    rng = np.random.default_rng(4097)
+    f = rng.standard_normal((1, N, N))
+    geo, _ = orc.square_geometry(N, np.float64)
+    bc = rng.random((1, N, N)) * (1 - geo)
+    mg_o = orc.OracleMultigrid(n, "poisson", np.float64)
+    mg_o.set_boundary(geo, bc)
+    s = MultigridSolver(n, dtype=torch.float64)
+    assert s.levels[0].f.numel() * 8 > 64 << 20  # the nontemporal instantiations run
+    s.set_boundary(torch.from_numpy(bc).cuda().reshape(1, 1, N, N))
+    s.set_rhs(f=torch.from_numpy(f).cuda().reshape(1, 1, N, N))
+    s.load()
+    v = bc.copy()
+    r0 = float(mg_o.residual_norm(v, f)[0])
+    s.vcycle()
+    v = mg_o.step(v, f)
+    got = s.solution().cpu().numpy()[:, 0]
+    err = np.abs(got - v).max() / np.abs(v).max()
+    assert err < 1e-10, f"first cycle: {err:.3e}"
+    s.vcycle(3)
+    for _ in range(3):
+        v = mg_o.step(v, f)
+    got = s.solution().cpu().numpy()[:, 0]
+    err = np.abs(got - v).max() / np.abs(v).max()
+    assert err < 1e-10, f"joined cycles 2-4: {err:.3e}"
+    res = float(s.residual_norm()[0])
+    ref = float(mg_o.residual_norm(v, f)[0])
+    assert abs(res - ref) <= 1e-9 * ref + 1e-12 * r0, (res, ref)
 
 
 def test_vcycle_graph_replay_matches_eager():
@@ -537,7 +616,7 @@ def test_vcycle_rect_vs_oracle(T, m, n, tail):
                                            ("poisson", 128, 512, 1), ("interface", 256, None, 2),
                                            ("poisson", 4, None, 1), ("poisson", 64, 8, 3)])
 @pytest.mark.parametrize("k", [2, 3, 6])
-def test_cycle_join_bitwise(T, problem, n, m, B, k):
+def test_cycle_join_bitwise(T, problem, n, m, B, k, nt):
     """vcycle(k) with the finest level's cycle boundaries joined (fea_mg_cycle_join) is bitwise the
     unjoined sequence of k V-cycles; the graph-replayed second call as well."""
     from feanet_amd.solver import MultigridSolver
@@ -577,7 +656,7 @@ def test_cycle_join_bitwise_full_size():
     assert torch.equal(out[0], out[1])
 
 
-def test_cycle_join_kernel_direct():
+def test_cycle_join_kernel_direct(nt):
     """fea_mg_cycle_join against fea_mg_prolong_sweep + fea_mg_sweep_restrict on random data, including
     boundary nodes that are not zero (Dirichlet data) and a coarse correction with a nonzero ring."""
     from feanet_amd import _lib

@@ -28,6 +28,21 @@ def test_pattern_maps_match_oracle_large():
         np.testing.assert_array_equal(ms.interface_pattern_map(257, shape), pid)
 
 
+def test_c3_maps_fixture_is_oracle(gold):
+    """Config C3 (2049^2 two-material): the oracle's element/node loop at the full size equals the
+    fixture the C3 GPU test builds its oracle hierarchy from, and the product's vectorised builder
+    equals the fixture on every level of the hierarchy (2049^2 .. 3^2).  ~70 s (the loop)."""
+    maps = gold("c3_pattern_maps.npz")
+    ktab, pid = orc.interface_mesh(2049, (1, 20), 0)
+    np.testing.assert_array_equal(pid, maps["pid_2049"])
+    np.testing.assert_array_equal(ktab, maps["ktab"])
+    np.testing.assert_array_equal(ms.stencil_table((1, 20)), maps["ktab"])
+    N = 2049
+    while N >= 3:
+        np.testing.assert_array_equal(ms.interface_pattern_map(N, 0), maps[f"pid_{N}"], err_msg=f"N={N}")
+        N = (N + 1) // 2
+
+
 def test_mass_stencil(gold):
     t = gold("tables.npz")
     for n in (2, 4, 16, 32, 64, 128, 4096):
