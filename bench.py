@@ -112,7 +112,7 @@ def time_fine_kernels(s, reps):
     args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), p0, kt, om, nt) + geom
     out["fea_mg_sweep"] = (time_kernel("mg_sweep", s.dtype, args, reps, st), (3 * es + pb) * nodes)
     args = (L0.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), L1.f.data_ptr(), p0, kt, om, nt,
-            s.rtab.data_ptr(), nr, s.w[0]) + geom + (L1.ld, L1.bs)
+            s.rtab.data_ptr(), nr, s.w[0]) + geom + (L1.ld, L1.bs, None, None, None)
     out["fea_mg_sweep_restrict"] = (time_kernel("mg_sweep_restrict", s.dtype, args, reps, st),
                                     (3 * es + pb) * nodes + es * cnodes)
     args = (L0.a.data_ptr(), L1.a.data_ptr(), L0.f.data_ptr(), L0.b.data_ptr(), p0, p1, kt, om, nt,

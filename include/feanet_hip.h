@@ -46,7 +46,8 @@ extern "C" {
 /* ---------------------------------------------------------------------------
  * Library / layout queries
  * ------------------------------------------------------------------------- */
-/* ABI version (bumped on any signature change; 2 = H x W framed grids). */
+/* ABI version (bumped on any signature change; 2 = H x W framed grids, 3 = fused residual norms of
+ * fea_mg_cycle_join / fea_mg_sweep_restrict). */
 int fea_abi_version(void);
 
 /* Framed layout of an H x W level for elements of `elem_size` bytes (4 or 8):
@@ -191,7 +192,8 @@ size_t fea_transfer_weight_grad_ws_bytes_f64(int C, int B, int Hc, int Wc);
  *     `pid`/`pidc` are framed uint8 maps with the same ld (in bytes) as the T fields.
  * ------------------------------------------------------------------------- */
 
-/* contiguous [B,1,H,W] -> framed, applying u*geo + bc (geo NULL: square, bc NULL: zero) */
+/* contiguous [B,1,H,W] -> framed, applying u*geo + bc (src NULL: u = 0; geo NULL: the square geometry,
+ * or all ones if geo_bstride < 0 (a raw copy); bc NULL: zero) */
 int fea_mg_pack_f32(const float* src, float* dst, const float* geo, long long geo_bstride,
                     const float* bc, long long bc_bstride, int B, int H, int W, int ld, long long bstride,
                     void* stream);
@@ -225,15 +227,18 @@ int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out
 
 /* Fused pre-smooth + residual + restriction on a level with a given iterate (temporal blocking):
  *   u_out = J(u, f) (interior)   and   fc(interior) = w0 * R(f - K u_out)
- * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357). */
+ * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357).
+ * norm_hist != NULL: also the residual norm ||(f - K u)[b, 1:-1, 1:-1]||_2 of the INPUT iterate (the
+ * drivers' initial residual, M-FEANet-mg_test.ipynb:27428-27429), appended to norm_hist as for
+ * fea_mg_cycle_join below. */
 int fea_mg_sweep_restrict_f32(const float* u, const float* f, float* u_out, float* fc, const uint8_t* pid,
                               const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
                               float w0, int B, int H, int W, int ld, long long bstride, int ldc, long long bstridec,
-                              void* stream);
+                              double* norm_ws, double* norm_hist, unsigned* norm_cnt, void* stream);
 int fea_mg_sweep_restrict_f64(const double* u, const double* f, double* u_out, double* fc, const uint8_t* pid,
                               const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
                               double w0, int B, int H, int W, int ld, long long bstride, int ldc, long long bstridec,
-                              void* stream);
+                              double* norm_ws, double* norm_hist, unsigned* norm_cnt, void* stream);
 
 /* Fused prolongation + correction + post-sweep:
  *   out = J(u + w1 * P(ec), f)   (P kernel by coarse-node pattern pidc)
@@ -253,15 +258,23 @@ int fea_mg_prolong_sweep_f64(const double* u, const double* ec, const double* f,
  * pre-smooth + residual + restriction of cycle k+1 in one pass —
  *   v = J(u + w1 * P(ec), f)  (not stored);   u_out = J(v, f);   fc(interior) = w0 * R(f - K u_out)
  * bitwise equal to fea_mg_prolong_sweep followed by fea_mg_sweep_restrict (FEANet/multigrid.py:177-181
- * then :165-170), reading u, f, ec once and writing u_out, fc (28 instead of 52 B per fp64 node). */
+ * then :165-170), reading u, f, ec once and writing u_out, fc (28 instead of 52 B per fp64 node).
+ * norm_hist != NULL: also the drivers' residual norm of v, the end-of-cycle-k iterate
+ * (||(f - K v)[b, 1:-1, 1:-1]||_2, M-FEANet-mg_test.ipynb:27428-27429), which the pre-smooth forms
+ * anyway: appended as row norm_cnt[1] of norm_hist (B doubles per row; norm_cnt[1] += 1; norm_cnt[0]
+ * unused), reduced deterministically by a one-workgroup kernel launched after the join on the same
+ * stream; norm_ws >= fea_norm_workspace_bytes(B, H, W).  Replaces the per-cycle residual pass of the driver
+ * loops (M-FEANet-mg_test.ipynb:27426-27436). */
 int fea_mg_cycle_join_f32(const float* u, const float* ec, const float* f, float* u_out, float* fc,
                           const uint8_t* pid, const uint8_t* pidc, const float* ktab, const float* omd, int ntab,
                           const float* ptab, int nptab, const float* rtab, int nrtab, float w1, float w0, int B,
-                          int H, int W, int ld, long long bstride, int ldc, long long bstridec, void* stream);
+                          int H, int W, int ld, long long bstride, int ldc, long long bstridec, double* norm_ws,
+                          double* norm_hist, unsigned* norm_cnt, void* stream);
 int fea_mg_cycle_join_f64(const double* u, const double* ec, const double* f, double* u_out, double* fc,
                           const uint8_t* pid, const uint8_t* pidc, const double* ktab, const double* omd, int ntab,
                           const double* ptab, int nptab, const double* rtab, int nrtab, double w1, double w0, int B,
-                          int H, int W, int ld, long long bstride, int ldc, long long bstridec, void* stream);
+                          int H, int W, int ld, long long bstride, int ldc, long long bstridec, double* norm_ws,
+                          double* norm_hist, unsigned* norm_cnt, void* stream);
 
 /* Prolongation + correction without a sweep (nu2 = 0 schedules): out = u + w1 * P(ec), interior. */
 int fea_mg_prolong_add_f32(const float* u, const float* ec, float* out, const uint8_t* pidc, const float* ptab,

@@ -273,6 +273,40 @@ __device__ __forceinline__ TaskId decode_task(int nstrips, int ntr) {
   return id;
 }
 
+// Fused residual norm of a launch (kernels with a NORM variant): every wave's partial sum of squares
+// goes to part[remapped block * kWaves + wave] (waves without a task write 0); k_norm_append, launched
+// right after on the same stream, sums each sample's partials in index order — deterministic, the same
+// order every launch — and appends sqrt(sum) as history row cnt[1].  (A last-workgroup reduction inside
+// the kernel would need a device-scope release per workgroup, i.e. an L2 write-back on every one of
+// them; the kernel boundary gives the same visibility once.)
+template <typename T>
+__device__ __forceinline__ void norm_partial(const MgArgs<T>& g, double ssq) {
+  ssq = wave_sum(ssq);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  if (lane_id() == 0) g.part[(long long)bid * kWaves + (threadIdx.x >> 6)] = ssq;
+}
+
+// One workgroup: hist[row * B + b] = sqrt(sum of part[b * per .. (b+1) * per - 1]) for row = cnt[1],
+// then cnt[1] = row + 1.
+__global__ __launch_bounds__(256) void k_norm_append(const double* __restrict__ part, long long per, int B,
+                                                    double* __restrict__ hist, unsigned* __restrict__ cnt) {
+  __shared__ double red[256];
+  const unsigned row = cnt[1];
+  for (int b = 0; b < B; ++b) {
+    double s = 0.0;
+    for (long long i = threadIdx.x; i < per; i += 256) s += part[b * per + i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) hist[(long long)row * B + b] = sqrt(red[0]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cnt[1] = row + 1;
+}
+
 // Loads ktab/omd (stride 10) and optionally a second 9-wide table into LDS.
 template <typename T>
 __device__ __forceinline__ void load_tables(T* tab, const T* ktab, const T* omd, int ntab, T* tab2,
@@ -611,20 +645,16 @@ __device__ __forceinline__ PRow<V> own_prow(const int (&x)[V]) {
   return w;
 }
 
-template <typename T, bool MULTI, bool NT>
-__global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
+// One row task of the sweep + restriction (below).  NORM: also accumulates, into ssq, the squared
+// residual f - K u of the INPUT iterate over the task's owned interior nodes (the sweep forms it):
+// the drivers' initial residual norm (M-FEANet-mg_test.ipynb:27428-27429) at no extra pass.
+template <typename T, bool MULTI, bool NT, bool NORM>
+__device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const TaskId& id, const T* tab,
+                                                    const T* rtb, double& ssq) {
   using F = Frame<T>;
   using O = Ovl<T>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
-  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  if constexpr (MULTI) {
-    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
-    __syncthreads();
-  }
-  const TaskId id = decode_task(g.nstrips, g.ntr);
-  if (!id.valid) return;
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
   const int c0 = 1 + id.s * O::S;  // first owned fine column
@@ -682,20 +712,24 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
     if constexpr (MULTI) w.p = own_prow<V>(r.p);
     return w;
   };
+  auto owns = [&](int y) { return own && y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2; };
   // u'(y) on the lane's own columns (boundary rows / columns keep u)
   auto usweep = [&](const Wn& a, const Wn& b, const Wn& c, int y, T (&o)[V]) {
     const bool rin = y >= 1 && y <= H - 2;
+    const bool count = NORM && owns(y);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acc = kapply<T, V, MULTI>(a.u, b.u, c.u, a.p, b.p, c.p, k, ks, tab);
       const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
-      const T v = omk * (b.f[k] - acc) + b.u.a[k + 1];
+      const T rr = b.f[k] - acc;
+      const T v = omk * rr + b.u.a[k + 1];
       o[k] = (rin && cin[k]) ? v : b.u.a[k + 1];
+      if constexpr (NORM)
+        if (count && rin && cin[k]) ssq += (double)rr * (double)rr;
     }
   };
   auto store_u = [&](int y, const T (&o)[V]) {
-    const bool ownr = y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2;
-    if (own && ownr) store_masked<T, V, NT>(ob + rowo(y), o, cl, W);
+    if (owns(y)) store_masked<T, V, NT>(ob + rowo(y), o, cl, W);
   };
   // residual row y (u' windows a, b, c; f and patterns of row y) -> restriction row ky into acc
   auto racc = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const Wn& sy, const Wn& pa,
@@ -773,6 +807,20 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
     X4 = X6;
     nB = m2;
   }
+}
+
+template <typename T, bool MULTI, bool NORM, bool NT>
+__global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  double ssq = 0.0;
+  if (id.valid) sweep_restrict_task<T, MULTI, NT, NORM>(g, id, tab, rtb, ssq);
+  if constexpr (NORM) norm_partial<T>(g, ssq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1055,27 +1103,18 @@ struct Ovl3 {
   static constexpr int OWN = S / V;                      // owning lanes L0 .. L0 + OWN - 1
 };
 
-template <typename T, bool MULTI, bool NT>
-__global__ __launch_bounds__(256)
-#if FEA_JOIN_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(FEA_JOIN_WAVES)))
-#endif
-void k_mg_cycle_join(MgArgs<T> g) {
+// One row task of the cycle join (below).  NORM: also accumulates, into ssq, the squared residual
+// f - K v of the post-smoothed iterate v (the end-of-cycle iterate the reference drivers measure,
+// M-FEANet-mg_test.ipynb:27428-27429) over the task's owned interior nodes — the pre-smooth of the
+// next cycle forms exactly that residual, so the norm costs no extra pass.
+template <typename T, bool MULTI, bool NT, bool NORM>
+__device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* rtb,
+                                          const T* ptb, double& ssq) {
   constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
   using F = Frame<T>;
   using O = Ovl3<T>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
-  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  if constexpr (MULTI) {
-    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
-    load_tables<T>(ptb, g.ptab, nullptr, g.nptab, nullptr, nullptr, 0);
-    __syncthreads();
-  }
-  const TaskId id = decode_task(g.nstrips, g.ntr);
-  if (!id.valid) return;
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
   const int c0 = 1 + id.s * O::S;  // first owned fine column (odd)
@@ -1144,16 +1183,20 @@ void k_mg_cycle_join(MgArgs<T> g) {
   CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(ys / 2 + 1));
   RawC<T, V> nC = rc(ys / 2 + 2);
 
+  // count: add the squared residual of the input row y to ssq (NORM; the row and lane own y)
   auto sweep_own = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
                        const PRow<V>& pb_, const PRow<V>& pc, const T (&fy)[V], const T (&keep)[V], int y,
-                       T (&o)[V]) {
+                       T (&o)[V], bool count) {
     const bool rin = y >= 1 && y <= H - 2;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acck = kapply<T, V, MULTI>(a, b, c, pa, pb_, pc, k, ks, tab);
       const T omk = MULTI ? tab[pb_.a[k + 1] + 9] : om;
-      const T v = omk * (fy[k] - acck) + b.a[k + 1];
+      const T rr = fy[k] - acck;
+      const T v = omk * rr + b.a[k + 1];
       o[k] = (rin && cin[k]) ? v : keep[k];
+      if constexpr (NORM)
+        if (count && rin && cin[k]) ssq += (double)rr * (double)rr;
     }
   };
 
@@ -1203,7 +1246,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
     // 2. v(y-1) = J(x) (boundary nodes keep u)
     if (y >= ys + 2) {
       T v[V];
-      sweep_own(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - 1, v);
+      sweep_own(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - 1, v, false);
       Va = Vb;
       Vb = Vc;
       Vc = own_row<T, V>(v);
@@ -1212,9 +1255,9 @@ void k_mg_cycle_join(MgArgs<T> g) {
         T keep[V], w[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) keep[k] = Vb.a[k + 1];
-        sweep_own(Va, Vb, Vc, P3, P2, P1, f1, keep, y - 2, w);
         const int yw = y - 2;
         const bool ownr = yw >= 2 * I0 - 1 && (yw < 2 * I1 - 1 || I1 == Hc - 1) && yw <= H - 2;
+        sweep_own(Va, Vb, Vc, P3, P2, P1, f1, keep, y - 2, w, own && ownr);
         if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, W);
         Wa = Wb;
         Wb = Wc_;
@@ -1287,6 +1330,26 @@ void k_mg_cycle_join(MgArgs<T> g) {
   if (y <= ye) step(y, std::integral_constant<int, 0>{});
   if (y + 1 <= ye) step(y + 1, std::integral_constant<int, 1>{});
   if (y + 2 <= ye) step(y + 2, std::integral_constant<int, 2>{});
+}
+
+template <typename T, bool MULTI, bool NORM, bool NT>
+__global__ __launch_bounds__(256)
+#if FEA_JOIN_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(FEA_JOIN_WAVES)))
+#endif
+void k_mg_cycle_join(MgArgs<T> g) {
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    load_tables<T>(ptb, g.ptab, nullptr, g.nptab, nullptr, nullptr, 0);
+    __syncthreads();
+  }
+  const TaskId id = decode_task(g.nstrips, g.ntr);
+  double ssq = 0.0;
+  if (id.valid) join_task<T, MULTI, NT, NORM>(g, id, tab, rtb, ptb, ssq);
+  if constexpr (NORM) norm_partial<T>(g, ssq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1369,8 +1432,9 @@ __global__ __launch_bounds__(256) void k_mg_pack(const T* __restrict__ src, T* _
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), r = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
   if (r >= H || c >= W) return;
   const long long i = (long long)r * W + c;
-  const T v = src[(long long)b * H * W + i];
-  const T gv = geo ? geo[b * geo_bs + i] : T((r > 0 && r < H - 1 && c > 0 && c < W - 1) ? 1 : 0);
+  const T v = src ? src[(long long)b * H * W + i] : T(0);
+  const T gv = geo ? geo[b * geo_bs + i]
+                   : T((geo_bs < 0 || (r > 0 && r < H - 1 && c > 0 && c < W - 1)) ? 1 : 0);
   const T bv = bc ? bc[b * bc_bs + i] : T(0);
   dst[(long long)b * bs + (long long)(r + 1) * ld + Frame<T>::OFF + c] = v * gv + bv;
 }
@@ -1492,7 +1556,7 @@ static inline dim3 mg_grid(int B, int ntr, int nstrips) {
   return dim3((unsigned)(B * ntr * div_up(nstrips, kWaves)));
 }
 
-extern "C" int fea_abi_version(void) { return 2; }
+extern "C" int fea_abi_version(void) { return 3; }
 
 extern "C" int fea_mg_layout(int H, int W, int elem_size, int* ld, long long* bstride) {
   if (!mg_dims_ok(H, W) || !ld || !bstride) return FEA_EINVAL;
@@ -1513,7 +1577,11 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
   // generic: one partial per 64x4 block; framed: one per (strip, row task) at the fp32 strip width
   const long long gen = (long long)div_up(W, 64) * div_up(H, 4);
   const long long frm = (long long)div_up(W, 64) * div_up(H, 2);
-  return (size_t)B * (size_t)std::max(gen, frm) * sizeof(double);
+  // fused norms of the cycle join: one partial per wave of its grid (>= 2 fine rows per task, overlapped
+  // strips of >= 120 owned columns, 4 waves per workgroup)
+  const long long join = (long long)std::max(1, (H + 1) / 2 - 2) * div_up(div_up(std::max(W - 2, 1), 120), kWaves) *
+                         kWaves;
+  return (size_t)B * (size_t)std::max(std::max(gen, frm), join) * sizeof(double);
 }
 
 #define FEA_NT_LAUNCH(K, TARGS)                                   \
@@ -1531,7 +1599,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
 #define FEA_MG_API(SUF, T)                                                                                   \
   extern "C" int fea_mg_pack_##SUF(const T* src, T* dst, const T* geo, long long geo_bs, const T* bc,         \
                                    long long bc_bs, int B, int H, int W, int ld, long long bs, void* stream) { \
-    if (!src || !dst || B <= 0 || B > 65535 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;                \
+    if (!dst || B <= 0 || B > 65535 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;                        \
     k_mg_pack<T><<<dim3(div_up(W, 64), div_up(H, 4), B), 256, 0, (hipStream_t)stream>>>(src, dst, geo, geo_bs, \
                                                                                        bc, bc_bs, H, W, ld, bs); \
     FEA_LAUNCH_CHECK();                                                                                      \
@@ -1592,10 +1660,13 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
   extern "C" int fea_mg_sweep_restrict_##SUF(const T* u, const T* f, T* u_out, T* fc, const uint8_t* pid,       \
                                              const T* ktab, const T* omd, int ntab, const T* rtab, int nrtab,    \
                                              T w0, int B, int H, int W, int ld, long long bs, int ldc,          \
-                                             long long bsc, void* stream) {                                    \
+                                             long long bsc, double* norm_ws, double* norm_hist,                 \
+                                             unsigned* norm_cnt, void* stream) {                                \
     if (!u || !f || !u_out || !fc || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(H, W, ld, bs) ||       \
         u_out == u)                                                                                          \
       return FEA_EINVAL;                                                                                     \
+    const bool norm = norm_hist != nullptr;                                                                  \
+    if (norm && (!norm_ws || !norm_cnt)) return FEA_EINVAL;                                                  \
     if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || (nrtab != ntab && nrtab != 1))          \
       return FEA_EINVAL;                                                                                     \
@@ -1607,10 +1678,20 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.nstrips = div_up(W - 2, Ovl<T>::S);  /* overlapped strips */                                           \
     g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 3, pick_rb(B, g.nstrips, H - 2, 2 * kRB));                    \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
+    g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (ntab > 1) FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA true)                                           \
-    else FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA false)                                                   \
+    if (norm && (long long)grid.x * kWaves * 8 > (long long)fea_norm_workspace_bytes(B, H, W))               \
+      return FEA_EINVAL;                                                                                     \
+    if (ntab > 1) {                                                                                          \
+      if (norm) FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA true COMMA true)                                  \
+      else FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA true COMMA false)                                      \
+    } else {                                                                                                 \
+      if (norm) FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA false COMMA true)                                 \
+      else FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA false COMMA false)                                     \
+    }                                                                                                        \
+    if (norm)                                                                                                \
+      k_norm_append<<<1, 256, 0, s>>>(norm_ws, (long long)(grid.x / B) * kWaves, B, norm_hist, norm_cnt);    \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \
@@ -1660,9 +1741,12 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
   extern "C" int fea_mg_cycle_join_##SUF(const T* u, const T* ec, const T* f, T* u_out, T* fc, const uint8_t* pid, \
                                          const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab, \
                                          int nptab, const T* rtab, int nrtab, T w1, T w0, int B, int H, int W,     \
-                                         int ld, long long bs, int ldc, long long bsc, void* stream) {            \
+                                         int ld, long long bs, int ldc, long long bsc, double* norm_ws,          \
+                                         double* norm_hist, unsigned* norm_cnt, void* stream) {                  \
     if (!u || !ec || !f || !u_out || !fc || !ktab || !omd || !ptab || !rtab || B <= 0 || u_out == u)          \
       return FEA_EINVAL;                                                                                     \
+    const bool norm = norm_hist != nullptr;                                                                  \
+    if (norm && (!norm_ws || !norm_cnt)) return FEA_EINVAL;                                                  \
     if (!layout_ok<T>(H, W, ld, bs) || !coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                     \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nrtab != ntab && nrtab != 1) || (nptab != ntab && nptab != 1)) \
       return FEA_EINVAL;                                                                                     \
@@ -1675,10 +1759,20 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.nstrips = div_up(W - 2, Ovl3<T>::S);                                                                   \
     g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 7, pick_rb(B, g.nstrips, H - 2, join_max_rb()));             \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
+    g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (multi) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true)                                                  \
-    else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false)                                                       \
+    if (norm && (long long)grid.x * kWaves * 8 > (long long)fea_norm_workspace_bytes(B, H, W))               \
+      return FEA_EINVAL;                                                                                     \
+    if (multi) {                                                                                             \
+      if (norm) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true COMMA true)                                      \
+      else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true COMMA false)                                          \
+    } else {                                                                                                 \
+      if (norm) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA true)                                     \
+      else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA false)                                         \
+    }                                                                                                        \
+    if (norm)                                                                                                \
+      k_norm_append<<<1, 256, 0, s>>>(norm_ws, (long long)(grid.x / B) * kWaves, B, norm_hist, norm_cnt);    \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \

@@ -18,6 +18,7 @@ are the ones a caller asks for (e.g. `.item()` on the residual norm, as the refe
 """
 import math
 import os
+import time
 
 import numpy as np
 import torch
@@ -43,6 +44,7 @@ class _Level:
         self.a = torch.zeros(numel, dtype=dtype, device=device)
         self.b = torch.zeros(numel, dtype=dtype, device=device)
         self.zero = None
+        self.c = None  # third iterate buffer of the finest level (solve(): the block's start state)
         self.pid = None
         if pid_np is not None:
             off = 128 // esz - 1
@@ -57,10 +59,8 @@ class _Level:
                                             out=self.pid.data_ptr() + self.ld + off, ld=self.ld)
 
     def buf(self, name):
-        if name == "zero":
-            if self.zero is None:
-                self.zero = torch.zeros_like(self.a)
-            return self.zero
+        if name in ("zero", "c") and getattr(self, name) is None:
+            setattr(self, name, torch.zeros_like(self.a))
         return getattr(self, name)
 
     def view(self, t):
@@ -218,6 +218,12 @@ class MultigridSolver:
                               device=dev)
         self.norm_out = torch.zeros(self.B, dtype=torch.float64, device=dev)
         self._state = "a"
+        self._hist = None  # solve(): fused residual-norm history + counters (_ensure_hist)
+        self._cnt = None
+        self._hist_gen = 0
+        self._f1_snap = None
+        self._bc_version = object()  # identity changes with every set_boundary (third-buffer packing)
+        self._c_bc = None
         self._plans = {}
         self._graphs = {}
         self._eager_runs = {}
@@ -272,37 +278,36 @@ class MultigridSolver:
             if not torch.equal(g, sq):
                 raise NotImplementedError("MultigridSolver: only the square geometry (geo.py:13-30) is fused")
         self._bc = None if bc_value is None else self._check_field(bc_value, "boundary_value")
+        self._bc_version = object()
 
     def _pack(self, x, dst, geo=None, bc=None, reset=True):
+        """x (None: zeros) -> framed dst; reset: x*geo + bc (square geometry), else a raw copy."""
         Lv = self.levels[0]
-        gp, gs = (None, 0)
         bp, bs = (None, 0)
         if bc is not None:
             bp, bs = bc.data_ptr(), self.H * self.W
-        if reset:
-            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), gp, gs, bp, bs, *Lv.geom(),
-                      ops._stream(x))
-        else:  # raw copy: geometry = all ones
-            ones = torch.ones_like(x)
-            _lib.call("mg_pack", self.dtype, x.data_ptr(), dst.data_ptr(), ones.data_ptr(), self.H * self.W,
-                      None, 0, *Lv.geom(), ops._stream(x))
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.call("mg_pack", self.dtype, None if x is None else x.data_ptr(), dst.data_ptr(), None,
+                  0 if reset else -1, bp, bs, *Lv.geom(), stream)
 
     def load(self, u0=None):
         """Set the fine-grid iterate (reset_boundary applied: u*geo + bc, jacobi.py:27-29)."""
         L0 = self.levels[0]
         bc = getattr(self, "_bc", None)
-        if u0 is None:
-            u0 = torch.zeros((self.B, 1, self.H, self.W), dtype=self.dtype, device=self.device)
-        u0 = self._check_field(u0, "u0")
+        if u0 is not None:
+            u0 = self._check_field(u0, "u0")
         self._pack(u0, L0.a, bc=bc)
         self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
+        if L0.c is not None and self._c_bc is not self._bc_version:
+            self._pack(u0, L0.c, bc=bc)  # c only needs the Dirichlet values on its boundary nodes
+            self._c_bc = self._bc_version
         self._state = "a"
         if self.smoother == "hjac":
             # HRelax forms J(u) - u with the iterate the driver passed, before reset_boundary
             # (M-FEANet-mg_test.ipynb:151-153; the drivers pass un-reset zeros, :27478-27489): the
             # first sweep of the next V-cycle sees bc - u0 on the boundary nodes
             self._raw = torch.zeros_like(L0.a)
-            self._pack(u0, self._raw, reset=False)
+            self._pack(u0, self._raw, reset=False)  # u0 None: zeros
             self._hjac_first = True
 
     def solution(self):
@@ -414,7 +419,7 @@ class MultigridSolver:
                                              kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
         if kind == "sweep_restrict":
             return ("mg_sweep_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
-                                          kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
+                                          kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l) + (None, None, None))
         if kind == "prolong_sweep":
             return ("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
                                          pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l))
@@ -454,17 +459,20 @@ class MultigridSolver:
         return (self.join_cycles and self.smoother == "jac" and self.nu1 == 1 and self.nu2 == 1 and
                 self.compat is None and not self.zero_start and self.fuse and self.L >= 2)
 
-    def _join_call(self, pre, ec_ptr):
+    def _join_call(self, pre, ec_ptr, norm=False, out=None):
         """fea_mg_cycle_join: PS(0) of the cycle whose pre-smoothed iterate is in `pre`, fused with the
-        next cycle's SR(0); the new pre-smoothed iterate lands in the other buffer."""
+        next cycle's SR(0); the new pre-smoothed iterate lands in the other buffer.  norm: also append the
+        residual norm of the cycle's end iterate to the solve history (solve())."""
         lv = self.levels
         L0, L1 = lv[0], lv[1]
         pid = None if L0.pid is None else L0.pid.data_ptr()
         pidc = None if L1.pid is None else L1.pid.data_ptr()
-        return ("mg_cycle_join", (self._ptr(0, pre), ec_ptr, L0.f.data_ptr(), self._ptr(0, "b" if pre == "a" else "a"),
+        out = out or ("b" if pre == "a" else "a")
+        return ("mg_cycle_join", (self._ptr(0, pre), ec_ptr, L0.f.data_ptr(), self._ptr(0, out),
                                   L1.f.data_ptr(), pid, pidc, self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab,
                                   self.ptab.data_ptr(), self.ptab.shape[0], self.rtab.data_ptr(),
-                                  self.rtab.shape[0], self.w[1], self.w[0]) + L0.geom() + (L1.ld, L1.bs))
+                                  self.rtab.shape[0], self.w[1], self.w[0]) + L0.geom() + (L1.ld, L1.bs) +
+                ((self.ws.data_ptr(), self._hist.data_ptr(), self._cnt.data_ptr()) if norm else (None, None, None)))
 
     def _run_segment(self, key, launches):
         """Launch a fixed list of calls: eager the first time, then as a captured HIP graph."""
@@ -581,13 +589,22 @@ class MultigridSolver:
         return self.solution()
 
     def solve(self, u0=None, f=None, F=None, eps=1e-6, max_cycles=100, bc_value=None):
-        """Driver loop of the reference notebooks: V-cycles until max_b ||r_b|| <= eps.  Returns
-        (u [B,1,N,N], residual history list of per-sample numpy arrays, first entry = initial)."""
+        """Driver loop of the reference notebooks (M-FEANet-mg_test.ipynb:27426-27436,
+        MM_Model_convergence.ipynb:196-203): V-cycles until max_b ||r_b|| <= eps (at most max_cycles;
+        stops after a non-finite norm, :27434-27436).  Returns (u [B,1,N,N], residual history: list of
+        per-sample numpy arrays, first entry = the initial residual).
+
+        Joinable solvers (V(1,1) Jacobi) run the device-resident loop of _solve_joined: the residual
+        norm of every cycle comes out of the cycle join (fused, no extra pass) and the host looks at the
+        history once per block of cycles.  The result — iterate and history — is that of the per-cycle
+        loop (bitwise the same iterate; norms summed in another fixed order)."""
         if bc_value is not None:
             self.set_boundary(bc_value)
         if f is not None or F is not None:
             self.set_rhs(f=f, F=F)
         self.load(u0)
+        if self._joinable() and not getattr(self, "_hjac_first", False) and self.use_graph:
+            return self._solve_joined(eps, max_cycles, u0)
         hist = [self.residual_norm().cpu().numpy()]
         while hist[-1].max() > eps and len(hist) <= max_cycles:
             self.vcycle()
@@ -595,6 +612,139 @@ class MultigridSolver:
             if not np.all(np.isfinite(hist[-1])):
                 break
         return self.solution(), hist
+
+    SOLVE_BLOCK_MAX = 64  # cycles per host check of the solve loop
+
+    def _ensure_hist(self, rows):
+        """Device history of fused residual norms (rows of B) and the join's counters; captured solve
+        graphs hold these pointers, so a reallocation retires them (new generation in their keys)."""
+        if self._hist is None or self._hist.shape[0] < rows:
+            self._hist = torch.zeros((max(1024, rows), self.B), dtype=torch.float64, device=self.device)
+            self._cnt = torch.zeros(2, dtype=torch.int32, device=self.device)
+            self._hist_gen += 1
+
+    def _set_cnt(self, row):
+        """Join counters for the next norm-fused launch: arrival count 0, history row `row` (device-side
+        fills, no host synchronisation)."""
+        self._cnt[0].fill_(0)
+        self._cnt[1].fill_(row)
+
+    def _solve_joined(self, eps, max_cycles, u0=None):
+        """The solve loop on the device.  State between blocks ("mid-cycle"): the pre-smoothed iterate of
+        the next cycle in a finest-level buffer S, its restricted residual in f_1 — what a cycle join
+        leaves.  A block runs nb x [levels >= 1 of a cycle + the norm-fused cycle join] (graph blocks of
+        graph_blocks(nb)), its joins ping-ponging between the two finest-level buffers other than S (a
+        third buffer, so S survives the block untouched); join i appends ||r|| of the iterate at the end
+        of cycle i to the device history.  The host reads the block's norms once and
+          * stops at the first cycle j with max_b ||r_b|| <= eps (or a non-finite norm), as the reference;
+          * if j is the block's last cycle, its end iterate v_j (never stored by the join) is recomputed by
+            the last post-smooth PS(0) from the join's inputs, still intact: bitwise the unjoined result;
+          * if j is earlier (the contraction beat the prediction), the block is re-run from S to j (f_1 of
+            S from a copy taken at the block's start).
+        The initial norm comes from the first pre-smooth (fea_mg_sweep_restrict with the fused norm).
+        Block sizes: 3 cycles, then the predicted count to eps from the last contraction ratio (multigrid
+        contraction slows towards its asymptotic rate, so the prediction errs short: another block costs
+        one host round trip, an overshoot a re-run)."""
+        self._ensure_hist(max_cycles + 2)
+        L0, L1 = self.levels[0], self.levels[1]
+        if L0.c is None or self._c_bc is not self._bc_version:
+            L0.buf("c")
+            self._pack(None, L0.c, bc=getattr(self, "_bc", None))  # boundary values (interior: written first)
+            self._c_bc = self._bc_version
+
+        def stop(h):
+            return (not np.all(np.isfinite(h))) or h.max() <= eps
+
+        if max_cycles < 1:
+            return self.solution(), [self.residual_norm().cpu().numpy()]
+        s0 = self._state
+        plan, _ = self._plan(s0)
+        head, mid = plan[0], plan[1:-1]
+        ec_ptr = plan[-1][1][1]
+        gen = self._hist_gen
+        assert head[0] == "mg_sweep_restrict", head[0]
+        hargs = head[1][:-3] + (self.ws.data_ptr(), self._hist.data_ptr(), self._cnt.data_ptr())
+        self._set_cnt(0)
+        self._run_segment(("head", s0, gen), [(head[0], hargs)])  # pre-smooth + initial norm (row 0)
+        S = "b" if s0 == "a" else "a"
+        log = self._solve_log = []
+        trace = getattr(self, "_trace", False)  # diagnostics: synchronise and time every phase
+
+        def mark(what):
+            if trace:
+                torch.cuda.synchronize(self.device)
+                log.append((what, time.perf_counter()))
+        mark("head")
+
+        def run_joins(S, nb):
+            """nb norm-fused cycles from start buffer S; returns (last read buffer, last written)."""
+            X, Y = [x for x in "abc" if x != S]
+            G = 1 << (max(1, self.GRAPH_CYCLES).bit_length() - 1)
+            p, t, last = S, X, None
+            for blk in self.graph_blocks(nb, G):
+                # (first read, first write, second write) fixes the whole buffer sequence of the block
+                key = ("sblock", p, t, Y if t == X else X, blk, gen)
+                launches = []
+                for _ in range(blk):
+                    launches += mid + [self._join_call(p, ec_ptr, norm=True, out=t)]
+                    last, p, t = p, t, (Y if t == X else X)
+                self._run_segment(key, launches)
+            return last, p
+
+        hist = None
+        c = 0
+        q = None
+        while True:
+            h = float(hist[-1].max()) if hist is not None else float("inf")
+            if eps <= 0.0 or (q is not None and not 0.0 < q < 1.0):
+                nb = self.SOLVE_BLOCK_MAX
+            elif q is None:
+                nb = 3
+            else:
+                nb = int(math.ceil(math.log(eps / h) / math.log(q))) if h > eps else 1
+            nb = max(1, min(nb, self.SOLVE_BLOCK_MAX, max_cycles - c))
+            if nb > 1:  # f_1 of the start state: the joins overwrite it, a re-run needs it back
+                if self._f1_snap is None:
+                    self._f1_snap = torch.empty_like(L1.f)
+                self._f1_snap.copy_(L1.f)
+            last_read, end = run_joins(S, nb)
+            mark("joins")
+            log.append(("block", c, nb))
+            if hist is None:
+                rows = self._hist[0:1 + nb].cpu().numpy()
+                hist = [rows[0]]
+                if stop(hist[0]):  # the loaded guess already meets eps: no cycle at all
+                    self.load(u0)
+                    return self.solution(), hist
+                new = rows[1:]
+            else:
+                new = self._hist[c + 1:c + 1 + nb].cpu().numpy()
+            mark("read")
+            j = next((i for i in range(nb) if stop(new[i])), None)
+            if j is not None and j < nb - 1:  # converged inside the block: re-run S -> cycle c + j + 1
+                L1.f.copy_(self._f1_snap)
+                self._set_cnt(c + 1)
+                last_read, end = run_joins(S, j + 1)
+                log.append(("rerun", c, j + 1))
+                mark("rerun")
+            keep = nb if j is None else j + 1
+            hist += [new[i] for i in range(keep)]
+            c += keep
+            S = end
+            if j is not None or c >= max_cycles:
+                break
+            q = float(hist[-1].max() / hist[-2].max()) if hist[-2].max() > 0 else None
+        # v of the last cycle: PS(0) from the last join's inputs (its pre-smoothed iterate `last_read`, the
+        # level-1 correction untouched since), into a ping-pong buffer of the unjoined plans
+        D = "b" if last_read == "a" else "a"
+        name, args = self._plan("a")[0][-1]
+        args = (self._ptr(0, last_read), args[1], args[2], self._ptr(0, D)) + args[4:]
+        self._run_segment(("tail", last_read, D), [(name, args)])
+        self._state = D
+        mark("tail")
+        u = self.solution()
+        mark("solution")
+        return u, hist
 
     # ------------------------------------------------------------------ accounting
     def bytes_per_vcycle(self, k=1):
@@ -631,8 +781,11 @@ class MultigridSolver:
                 else:  # read f_a..f_{a+k-1}, u_{a+k}; write u_a
                     total += esz * (sum(sizes) + sizes[0]) + pb * sum(sizes)
                 continue
-            B, H, W = (args[-7:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add",
-                                               "mg_sweep_restrict") else args[-5:-2])
+            if name == "mg_sweep_restrict":  # (..., B, H, W, ld, bs, ldc, bsc, norm_ws, norm_hist, norm_cnt)
+                B, H, W = args[-10:-7]
+            else:
+                B, H, W = (args[-7:-4] if name in ("mg_residual_restrict", "mg_prolong_sweep", "mg_prolong_add")
+                           else args[-5:-2])
             nodes = B * (H - 2) * (W - 2)
             coarse = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
             if name == "mg_sweep":
