@@ -58,6 +58,16 @@ int fea_mg_layout(int H, int W, int elem_size, int* ld, long long* bstride);
 /* Bytes of double workspace needed by the norm kernels for this shape. */
 size_t fea_norm_workspace_bytes(int B, int H, int W);
 
+/* Fused residual norms, deferred: fea_mg_cycle_join with norm_ws != NULL and norm_hist == NULL only
+ * writes its per-wave partial sums of squares, fea_mg_join_norm_parts(B, H, W, elem_size) per sample
+ * (sample b at norm_ws[b * per ..]); fea_norm_append then reduces nrows such partial sets (set r at
+ * ws + r * stride, stride >= B * per doubles) in index order and appends sqrt as rows cnt[1] ..
+ * cnt[1] + nrows - 1 of hist (B doubles per row), cnt[1] += nrows.  A solve loop gives each joined cycle
+ * of a graph block its own partial set and reduces them with ONE launch at the block's end. */
+long long fea_mg_join_norm_parts(int B, int H, int W, int elem_size);
+int fea_norm_append(const double* ws, long long stride, long long per, int B, int nrows, double* hist,
+                    unsigned* cnt, void* stream);
+
 /* ---------------------------------------------------------------------------
  * (1) Generic ops, contiguous [B, C, H, W]
  * ------------------------------------------------------------------------- */

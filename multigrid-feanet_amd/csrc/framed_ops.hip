@@ -286,25 +286,28 @@ __device__ __forceinline__ void norm_partial(const MgArgs<T>& g, double ssq) {
   if (lane_id() == 0) g.part[(long long)bid * kWaves + (threadIdx.x >> 6)] = ssq;
 }
 
-// One workgroup: hist[row * B + b] = sqrt(sum of part[b * per .. (b+1) * per - 1]) for row = cnt[1],
-// then cnt[1] = row + 1.
-__global__ __launch_bounds__(256) void k_norm_append(const double* __restrict__ part, long long per, int B,
-                                                    double* __restrict__ hist, unsigned* __restrict__ cnt) {
+// One workgroup: for r < nrows, hist[(row0 + r) * B + b] = sqrt(sum of part[r * stride + b * per + i],
+// i < per) with row0 = cnt[1]; then cnt[1] = row0 + nrows.
+__global__ __launch_bounds__(256) void k_norm_append(const double* __restrict__ part, long long stride, long long per,
+                                                    int B, int nrows, double* __restrict__ hist,
+                                                    unsigned* __restrict__ cnt) {
   __shared__ double red[256];
-  const unsigned row = cnt[1];
-  for (int b = 0; b < B; ++b) {
-    double s = 0.0;
-    for (long long i = threadIdx.x; i < per; i += 256) s += part[b * per + i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+  const unsigned row0 = cnt[1];
+  for (int r = 0; r < nrows; ++r)
+    for (int b = 0; b < B; ++b) {
+      const double* p = part + r * stride + b * per;
+      double s = 0.0;
+      for (long long i = threadIdx.x; i < per; i += 256) s += p[i];
+      red[threadIdx.x] = s;
+      __syncthreads();
+      for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) hist[(long long)(row0 + r) * B + b] = sqrt(red[0]);
       __syncthreads();
     }
-    if (threadIdx.x == 0) hist[(long long)row * B + b] = sqrt(red[0]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) cnt[1] = row + 1;
+  if (threadIdx.x == 0) cnt[1] = row0 + nrows;
 }
 
 // Loads ktab/omd (stride 10) and optionally a second 9-wide table into LDS.
@@ -1584,6 +1587,36 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
   return (size_t)B * (size_t)std::max(std::max(gen, frm), join) * sizeof(double);
 }
 
+// launch configuration of the cycle join (overlapped strips, balanced row tasks)
+template <typename T>
+static void join_config(int B, int H, int W, MgArgs<T>& g) {
+  g.nstrips = div_up(W - 2, Ovl3<T>::S);
+  g.rb = balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, pick_rb(B, g.nstrips, H - 2, join_max_rb()));
+  g.ntr = div_up((H + 1) / 2 - 2, g.rb / 2);
+}
+
+extern "C" long long fea_mg_join_norm_parts(int B, int H, int W, int elem_size) {
+  if (B <= 0 || !mg_dims_ok(H, W) || !mg_odd(H, W)) return -1;
+  MgArgs<double> gd{};
+  MgArgs<float> gf{};
+  if (elem_size == 8) {
+    join_config<double>(B, H, W, gd);
+    return (long long)gd.ntr * div_up(gd.nstrips, kWaves) * kWaves;
+  }
+  if (elem_size == 4) {
+    join_config<float>(B, H, W, gf);
+    return (long long)gf.ntr * div_up(gf.nstrips, kWaves) * kWaves;
+  }
+  return -1;
+}
+
+extern "C" int fea_norm_append(const double* ws, long long stride, long long per, int B, int nrows, double* hist,
+                               unsigned* cnt, void* stream) {
+  if (!ws || !hist || !cnt || B <= 0 || nrows <= 0 || per <= 0 || (nrows > 1 && stride < B * per)) return FEA_EINVAL;
+  k_norm_append<<<1, 256, 0, (hipStream_t)stream>>>(ws, stride, per, B, nrows, hist, cnt);
+  FEA_LAUNCH_CHECK();
+}
+
 #define FEA_NT_LAUNCH(K, TARGS)                                   \
   {                                                               \
     if (g.nt) K<TARGS, true><<<grid, 256, 0, s>>>(g);             \
@@ -1691,7 +1724,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
       else FEA_NT_LAUNCH(k_mg_sweep_restrict, T COMMA false COMMA false)                                     \
     }                                                                                                        \
     if (norm)                                                                                                \
-      k_norm_append<<<1, 256, 0, s>>>(norm_ws, (long long)(grid.x / B) * kWaves, B, norm_hist, norm_cnt);    \
+      k_norm_append<<<1, 256, 0, s>>>(norm_ws, 0, (long long)(grid.x / B) * kWaves, B, 1, norm_hist, norm_cnt); \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   static int mg_prolong_##SUF(const T* u, const T* ec, const T* f, T* out, const uint8_t* pid,               \
@@ -1745,8 +1778,8 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
                                          double* norm_hist, unsigned* norm_cnt, void* stream) {                  \
     if (!u || !ec || !f || !u_out || !fc || !ktab || !omd || !ptab || !rtab || B <= 0 || u_out == u)          \
       return FEA_EINVAL;                                                                                     \
-    const bool norm = norm_hist != nullptr;                                                                  \
-    if (norm && (!norm_ws || !norm_cnt)) return FEA_EINVAL;                                                  \
+    const bool norm = norm_ws != nullptr, append = norm_hist != nullptr;                                      \
+    if (append && (!norm_ws || !norm_cnt)) return FEA_EINVAL;                                                \
     if (!layout_ok<T>(H, W, ld, bs) || !coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                     \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nrtab != ntab && nrtab != 1) || (nptab != ntab && nptab != 1)) \
       return FEA_EINVAL;                                                                                     \
@@ -1756,9 +1789,7 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
     g.u = u; g.ec = ec; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.pidc = pidc; g.ktab = ktab;       \
     g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;     \
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
-    g.nstrips = div_up(W - 2, Ovl3<T>::S);                                                                   \
-    g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 7, pick_rb(B, g.nstrips, H - 2, join_max_rb()));             \
-    g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
+    join_config<T>(B, H, W, g);                                                                              \
     g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
@@ -1771,8 +1802,8 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
       if (norm) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA true)                                     \
       else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA false)                                         \
     }                                                                                                        \
-    if (norm)                                                                                                \
-      k_norm_append<<<1, 256, 0, s>>>(norm_ws, (long long)(grid.x / B) * kWaves, B, norm_hist, norm_cnt);    \
+    if (append)                                                                                              \
+      k_norm_append<<<1, 256, 0, s>>>(norm_ws, 0, (long long)(grid.x / B) * kWaves, B, 1, norm_hist, norm_cnt); \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
   extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \

@@ -57,6 +57,8 @@ _EXTRA = {
     "fea_abi_version": ([], I),
     "fea_mg_layout": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(LL)], I),
     "fea_norm_workspace_bytes": ([I, I, I], ctypes.c_size_t),
+    "fea_mg_join_norm_parts": ([I, I, I, I], LL),
+    "fea_norm_append": ([P, LL, LL, I, I, P, P, P], I),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
     "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
     "fea_interface_pattern_map": ([P, LL, I, I, F64, P], I),
@@ -110,6 +112,18 @@ def call(name, dtype, *args):
     if rc != 0:
         what = "invalid arguments" if rc == -1 else f"hipError_t {rc}"
         raise RuntimeError(f"feanet_amd: fea_{name}_{suf} failed ({what})")
+
+
+def call_raw(name, *args):
+    """Invoke a dtype-free entry point fea_<name> (e.g. norm_append); RuntimeError on a nonzero return."""
+    rc = getattr(lib(), f"fea_{name}")(*args)
+    if rc != 0:
+        raise RuntimeError(f"feanet_amd: fea_{name} failed ({'invalid arguments' if rc == -1 else f'hipError_t {rc}'})")
+
+
+def join_norm_parts(B, H, W, elem_size):
+    """Per-sample partial sums the cycle join writes in its deferred-norm mode."""
+    return int(lib().fea_mg_join_norm_parts(B, H, W, elem_size))
 
 
 def mg_layout(H, W, elem_size):

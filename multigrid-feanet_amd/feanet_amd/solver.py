@@ -222,6 +222,7 @@ class MultigridSolver:
         self._cnt = None
         self._hist_gen = 0
         self._f1_snap = None
+        self._sws = None  # solve(): per-cycle partial norm sets of a graph block
         self._bc_version = object()  # identity changes with every set_boundary (third-buffer packing)
         self._c_bc = None
         self._plans = {}
@@ -453,13 +454,16 @@ class MultigridSolver:
     def _launch(self, plan):
         stream = torch.cuda.current_stream(self.device).cuda_stream
         for name, args in plan:
-            _lib.call(name, self.dtype, *args, stream)
+            if name == "norm_append":  # dtype-free entry point
+                _lib.call_raw(name, *args, stream)
+            else:
+                _lib.call(name, self.dtype, *args, stream)
 
     def _joinable(self):
         return (self.join_cycles and self.smoother == "jac" and self.nu1 == 1 and self.nu2 == 1 and
                 self.compat is None and not self.zero_start and self.fuse and self.L >= 2)
 
-    def _join_call(self, pre, ec_ptr, norm=False, out=None):
+    def _join_call(self, pre, ec_ptr, norm=False, out=None, norm_ws=None):
         """fea_mg_cycle_join: PS(0) of the cycle whose pre-smoothed iterate is in `pre`, fused with the
         next cycle's SR(0); the new pre-smoothed iterate lands in the other buffer.  norm: also append the
         residual norm of the cycle's end iterate to the solve history (solve())."""
@@ -472,7 +476,8 @@ class MultigridSolver:
                                   L1.f.data_ptr(), pid, pidc, self.ktab.data_ptr(), self.omd.data_ptr(), self.ntab,
                                   self.ptab.data_ptr(), self.ptab.shape[0], self.rtab.data_ptr(),
                                   self.rtab.shape[0], self.w[1], self.w[0]) + L0.geom() + (L1.ld, L1.bs) +
-                ((self.ws.data_ptr(), self._hist.data_ptr(), self._cnt.data_ptr()) if norm else (None, None, None)))
+                ((norm_ws, None, None) if norm_ws is not None else
+                 (self.ws.data_ptr(), self._hist.data_ptr(), self._cnt.data_ptr()) if norm else (None, None, None)))
 
     def _run_segment(self, key, launches):
         """Launch a fixed list of calls: eager the first time, then as a captured HIP graph."""
@@ -623,6 +628,16 @@ class MultigridSolver:
             self._cnt = torch.zeros(2, dtype=torch.int32, device=self.device)
             self._hist_gen += 1
 
+    def _read_hist(self, r0, r1):
+        """History rows r0..r1-1 to the host: one async copy into pinned memory, then a stream sync."""
+        n = (r1 - r0) * self.B
+        if getattr(self, "_hist_host", None) is None or self._hist_host.numel() < self._hist.numel():
+            self._hist_host = torch.empty(self._hist.numel(), dtype=torch.float64, pin_memory=True)
+        out = self._hist_host[:n]
+        out.copy_(self._hist[r0:r1].reshape(-1), non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return out.numpy().reshape(r1 - r0, self.B).copy()
+
     def _set_cnt(self, row):
         """Join counters for the next norm-fused launch: arrival count 0, history row `row` (device-side
         fills, no host synchronisation)."""
@@ -642,9 +657,9 @@ class MultigridSolver:
           * if j is earlier (the contraction beat the prediction), the block is re-run from S to j (f_1 of
             S from a copy taken at the block's start).
         The initial norm comes from the first pre-smooth (fea_mg_sweep_restrict with the fused norm).
-        Block sizes: 3 cycles, then the predicted count to eps from the last contraction ratio (multigrid
-        contraction slows towards its asymptotic rate, so the prediction errs short: another block costs
-        one host round trip, an overshoot a re-run)."""
+        Block sizes: 3 cycles, then the predicted count to eps from the last contraction ratio plus its
+        last increase (V-cycle contraction grows towards its asymptotic rate; the extrapolation is bounded
+        so the prediction errs short: another block costs one host round trip, an overshoot a re-run)."""
         self._ensure_hist(max_cycles + 2)
         L0, L1 = self.levels[0], self.levels[1]
         if L0.c is None or self._c_bc is not self._bc_version:
@@ -664,9 +679,19 @@ class MultigridSolver:
         gen = self._hist_gen
         assert head[0] == "mg_sweep_restrict", head[0]
         hargs = head[1][:-3] + (self.ws.data_ptr(), self._hist.data_ptr(), self._cnt.data_ptr())
+        head_launch = (head[0], hargs)  # pre-smooth + initial norm (row 0): opens the first block's graph
         self._set_cnt(0)
-        self._run_segment(("head", s0, gen), [(head[0], hargs)])  # pre-smooth + initial norm (row 0)
         S = "b" if s0 == "a" else "a"
+        # deferred norms: each joined cycle of a graph block writes its partial sums to its own set, one
+        # reduction launch per graph block appends the block's rows
+        esz = 4 if self.dtype == torch.float32 else 8
+        per = _lib.join_norm_parts(self.B, L0.H, L0.W, esz)
+        stride = per * self.B
+        Gmax = self.SOLVE_BLOCK_MAX
+        if self._sws is None or self._sws.numel() < Gmax * stride:
+            self._sws = torch.zeros(Gmax * stride, dtype=torch.float64, device=self.device)
+            self._hist_gen += 1  # captured solve graphs hold the old workspace pointer
+            gen = self._hist_gen
         log = self._solve_log = []
         trace = getattr(self, "_trace", False)  # diagnostics: synchronise and time every phase
 
@@ -676,18 +701,28 @@ class MultigridSolver:
                 log.append((what, time.perf_counter()))
         mark("head")
 
-        def run_joins(S, nb):
-            """nb norm-fused cycles from start buffer S; returns (last read buffer, last written)."""
+        def run_joins(S, nb, with_head=False):
+            """nb norm-fused cycles from start buffer S (after the first pre-smooth if with_head), one graph
+            per block of up to SOLVE_BLOCK_MAX cycles; returns (last read buffer, last written)."""
             X, Y = [x for x in "abc" if x != S]
-            G = 1 << (max(1, self.GRAPH_CYCLES).bit_length() - 1)
             p, t, last = S, X, None
-            for blk in self.graph_blocks(nb, G):
+            for blk in ([nb] if nb <= Gmax else self.graph_blocks(nb, Gmax)):
                 # (first read, first write, second write) fixes the whole buffer sequence of the block
-                key = ("sblock", p, t, Y if t == X else X, blk, gen)
-                launches = []
-                for _ in range(blk):
-                    launches += mid + [self._join_call(p, ec_ptr, norm=True, out=t)]
+                key = ("sblock", with_head, p, t, Y if t == X else X, blk, gen)
+                g = self._graphs.get(key)
+                if g is not None:  # captured: replay without rebuilding the launch list
+                    for _ in range(blk):
+                        last, p, t = p, t, (Y if t == X else X)
+                    g.replay()
+                    with_head = False
+                    continue
+                launches = [head_launch] if with_head else []
+                with_head = False
+                for i in range(blk):  # cycle i of the graph block: partial sums into set i
+                    launches += mid + [self._join_call(p, ec_ptr, out=t, norm_ws=self._sws.data_ptr() + 8 * i * stride)]
                     last, p, t = p, t, (Y if t == X else X)
+                launches.append(("norm_append", (self._sws.data_ptr(), stride, per, self.B, blk, self._hist.data_ptr(),
+                                                 self._cnt.data_ptr())))
                 self._run_segment(key, launches)
             return last, p
 
@@ -703,28 +738,32 @@ class MultigridSolver:
             else:
                 nb = int(math.ceil(math.log(eps / h) / math.log(q))) if h > eps else 1
             nb = max(1, min(nb, self.SOLVE_BLOCK_MAX, max_cycles - c))
-            if nb > 1:  # f_1 of the start state: the joins overwrite it, a re-run needs it back
-                if self._f1_snap is None:
+            if nb > 1 and hist is not None:  # f_1 of the start state: the joins overwrite it, a re-run
+                if self._f1_snap is None:      # needs it back (the first block re-runs from u0 instead)
                     self._f1_snap = torch.empty_like(L1.f)
                 self._f1_snap.copy_(L1.f)
-            last_read, end = run_joins(S, nb)
+            last_read, end = run_joins(S, nb, with_head=hist is None)
             mark("joins")
             log.append(("block", c, nb))
             if hist is None:
-                rows = self._hist[0:1 + nb].cpu().numpy()
+                rows = self._read_hist(0, 1 + nb)
                 hist = [rows[0]]
                 if stop(hist[0]):  # the loaded guess already meets eps: no cycle at all
                     self.load(u0)
                     return self.solution(), hist
                 new = rows[1:]
             else:
-                new = self._hist[c + 1:c + 1 + nb].cpu().numpy()
+                new = self._read_hist(c + 1, c + 1 + nb)
             mark("read")
             j = next((i for i in range(nb) if stop(new[i])), None)
             if j is not None and j < nb - 1:  # converged inside the block: re-run S -> cycle c + j + 1
-                L1.f.copy_(self._f1_snap)
-                self._set_cnt(c + 1)
-                last_read, end = run_joins(S, j + 1)
+                if c == 0:
+                    self.load(u0)
+                    self._set_cnt(0)
+                else:
+                    L1.f.copy_(self._f1_snap)
+                    self._set_cnt(c + 1)
+                last_read, end = run_joins(S, j + 1, with_head=c == 0)
                 log.append(("rerun", c, j + 1))
                 mark("rerun")
             keep = nb if j is None else j + 1
@@ -733,7 +772,13 @@ class MultigridSolver:
             S = end
             if j is not None or c >= max_cycles:
                 break
-            q = float(hist[-1].max() / hist[-2].max()) if hist[-2].max() > 0 else None
+            rs = [float(hist[i + 1].max() / hist[i].max()) for i in (len(hist) - 3, len(hist) - 2)
+                  if i >= 0 and hist[i].max() > 0]
+            q = rs[-1] if rs else None
+            if len(rs) == 2 and q is not None:
+                # V-cycle contraction grows towards its asymptote: extrapolate the last step (bounded), so
+                # the prediction is not systematically one cycle short
+                q = min(q + max(0.0, rs[1] - rs[0]), 1.15 * q)
         # v of the last cycle: PS(0) from the last join's inputs (its pre-smoothed iterate `last_read`, the
         # level-1 correction untouched since), into a ping-pong buffer of the unjoined plans
         D = "b" if last_read == "a" else "a"

