@@ -16,14 +16,17 @@ Also reported on the same JSON line:
   north_star_kernel  the fine-level Ke-stencil Jacobi sweep fea_mg_sweep on its own (24 B per node:
                 read u, read f, write u'), back-to-back launches — the north star's >= 70 % target
   fine_level_kernels  the same measurement (isolated, back-to-back) for every level-0 kernel
-  cpu_baseline  the CPU oracle (numpy restatement of the reference V-cycle, 1 thread) on the same
-                workload, a bounded sample of whole V-cycles, rank 0 at N = 1 only.
+  cpu_baseline  the reference's PyTorch-CPU formulation (oracle/torch_cpu.py: conv2d / conv_transpose2d,
+                MultiGrid.Step) on the same workload with all of this job's host cores, a bounded sample
+                of whole V-cycles, rank 0 at N = 1 only (the 1-thread numpy oracle beside it).
 
-Multi-GPU (torchrun, one process per GPU): domain decomposition (feanet_amd.dd) of one global grid
-that grows with the GPU count at a fixed 4096 x 4096 intervals per GPU (weak scaling: 4097^2,
-8193x4097, 8193^2, 16385x8193 for 1, 2, 4, 8 GPUs), row slabs with RCCL halo exchange and an
-agglomerated coarse solve; value = global DoF / t_step.  --mode replicas runs independent
-problems instead.  Timing: barrier + synchronize on both sides of the K steps, max over ranks.
+Multi-GPU (torchrun, one process per GPU): domain decomposition (feanet_amd.dd) of ONE global grid,
+8193^2 by default (BASELINE config C4; strong scaling: the same grid over 2, 4, 8 GPUs), 2-D blocks
+(2x1, 2x2, 4x2) with a two-phase RCCL halo exchange once per V-cycle and an agglomerated coarse
+solve; value = global DoF / t_step.  --weak keeps 4096 x 4096 intervals per GPU instead (4097^2,
+8193x4097, 8193^2, 16385x8193); --mode replicas runs independent problems.  At N = 1 the default is
+the metric configuration (4097^2, one GPU, no decomposition).  Timing: barrier + synchronize on both
+sides of the K steps, max over ranks.
 """
 import argparse
 import json
@@ -257,6 +260,12 @@ def main():
     ap.add_argument("--mode", default=None, choices=["single", "dd", "replicas"],
                     help="default: single at 1 GPU, dd (domain decomposition, weak scaling) at N > 1")
     ap.add_argument("--agglomerate", type=int, default=None, help="dd: level gathered for the coarse solve")
+    ap.add_argument("--global-n", type=int, default=None,
+                    help="dd: intervals per edge of ONE global grid split over the ranks (strong scaling; default "
+                         "8192 = BASELINE config C4, 8193^2 over the GPUs)")
+    ap.add_argument("--weak", action="store_true",
+                    help="dd: weak scaling instead, --n x --n intervals per GPU (4097^2, 8193x4097, 8193^2, 16385x8193)")
+    ap.add_argument("--grid", default=None, help="dd: rank grid PRxPC (default: 2->2x1, 4->2x2, 8->4x2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     args = ap.parse_args()
@@ -271,9 +280,13 @@ def main():
     if mode == "dd":
         if args.problem != "poisson":
             raise SystemExit("bench: the domain-decomposed path runs the Poisson problem")
-        from feanet_amd.dd import DDSolver, TorchComm
-        m, nc = dd_domain(ws, n)
-        s = DDSolver(nc, m, rank, ws, comm=TorchComm(), agglomerate=args.agglomerate, dtype=T, batch=B)
+        from feanet_amd.dd import DDSolver, TorchComm, default_grid
+        if args.weak:
+            m, nc = dd_domain(ws, n)
+        else:
+            m = nc = args.global_n or 8192
+        grid = tuple(int(x) for x in args.grid.lower().split("x")) if args.grid else default_grid(ws)
+        s = DDSolver(nc, m, rank, ws, comm=TorchComm(), agglomerate=args.agglomerate, dtype=T, batch=B, grid=grid)
         g.manual_seed(1234)  # one global problem: every rank draws the same rhs and keeps its rows
         f = torch.randn(B, 1, m + 1, nc + 1, device="cuda", dtype=T, generator=g)
         s.set_rhs(f)
@@ -281,12 +294,13 @@ def main():
         torch.cuda.empty_cache()
         dof = B * (m + 1) * (nc + 1)
         lvl = s.local
-        p0 = s.parts[0]
+        p0, q0 = s.parts[0], s.cparts[0]
         workload = (f"{m + 1}x{nc + 1} poisson {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
-                    f"{ws} row slabs of {p0.e - p0.s} rows (+ghosts) x {nc + 1}, levels >= {s.Ld} agglomerated, "
-                    f"batch {B}")
-        parallelism = (f"dd{ws}: row slabs, RCCL halo exchange ({2 * s.Ld - 1} per V-cycle) + all-gather of "
-                       f"level {s.Ld}, redundant coarse solve")
+                    f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
+                    f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
+                    + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))
+        parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (x then y phase, depths "
+                       f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
     else:
         N = n + 1
         s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
@@ -364,7 +378,7 @@ def main():
         "warmup": warm,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if (mode == "dd" and not args.weak) else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded Gaussian rhs, zero initial guess)",

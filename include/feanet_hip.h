@@ -295,14 +295,15 @@ int fea_mg_prolong_add_f64(const double* u, const double* ec, double* out, const
                            int ldc, long long bstridec, void* stream);
 
 /* out[b] = || (f - K u)[b, rlo:rhi, 1:-1] ||_2 (rows rlo..rhi-1; rlo = rhi = 0: all interior rows,
- * the drivers' [1:-1, 1:-1]), deterministic; ws >= fea_norm_workspace_bytes(B, H, W).  A row range
- * gives a domain-decomposed rank the sum over the rows it owns. */
+ * the drivers' [1:-1, 1:-1]; likewise columns clo..chi-1, clo = chi = 0: all interior columns),
+ * deterministic; ws >= fea_norm_workspace_bytes(B, H, W).  Row and column ranges give a
+ * domain-decomposed rank the sum over the nodes it owns. */
 int fea_mg_residual_norm_f32(const float* u, const float* f, const uint8_t* pid, const float* ktab, int ntab,
                              double* out, double* ws, int B, int H, int W, int ld, long long bstride, int rlo,
-                             int rhi, void* stream);
+                             int rhi, int clo, int chi, void* stream);
 int fea_mg_residual_norm_f64(const double* u, const double* f, const uint8_t* pid, const double* ktab, int ntab,
                              double* out, double* ws, int B, int H, int W, int ld, long long bstride, int rlo,
-                             int rhi, void* stream);
+                             int rhi, int clo, int chi, void* stream);
 
 /* One sweep of the learned smoother (HJacIterator.HRelax, M-FEANet-mg_test.ipynb:147-155, HNet
  * :97-106) fused in one pass:  j = J(u, f);  d = (W_nl * .. (W_1 * (j - u)) .g ..) .g;  out = j + d

@@ -251,6 +251,7 @@ struct MgArgs {
   int nstrips, ntr;  // strips per row, row tasks per sample
   int rb;            // fine rows per row task (even)
   int rlo, rhi;      // row range of the residual norm
+  int clo, chi;      // column range of the residual norm
   int nt;            // nontemporal stores (level larger than FEANET_NT_BYTES)
 };
 
@@ -1409,7 +1410,7 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T rr = fv[k] - kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
-      if (cl + k <= W - 2) s += (double)rr * (double)rr;
+      if (cl + k >= g.clo && cl + k < g.chi) s += (double)rr * (double)rr;
     }
     w0 = w1;
     w1 = w2;
@@ -1539,6 +1540,8 @@ static MgArgs<T> mg_args(int H, int W, int ld, long long bs, int B) {
   g.ntr = div_up(H - 2, g.rb);
   g.rlo = 1;
   g.rhi = H - 1;
+  g.clo = 1;
+  g.chi = W - 1;
   return g;
 }
 
@@ -1808,7 +1811,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
   }                                                                                                          \
   extern "C" int fea_mg_residual_norm_##SUF(const T* u, const T* f, const uint8_t* pid, const T* ktab,        \
                                             int ntab, double* out, double* ws, int B, int H, int W, int ld,   \
-                                            long long bs, int rlo, int rhi, void* stream) {                  \
+                                            long long bs, int rlo, int rhi, int clo, int chi, void* stream) {\
     if (!u || !f || !ktab || !out || !ws || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;         \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
     if (rlo == 0 && rhi == 0) {                                                                              \
@@ -1816,9 +1819,14 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
       rhi = H - 1;                                                                                           \
     }                                                                                                        \
     if (rlo < 1 || rhi > H - 1 || rhi < rlo) return FEA_EINVAL;                                              \
+    if (clo == 0 && chi == 0) {                                                                              \
+      clo = 1;                                                                                               \
+      chi = W - 1;                                                                                           \
+    }                                                                                                        \
+    if (clo < 1 || chi > W - 1 || chi < clo) return FEA_EINVAL;                                              \
     MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.pid = pid; g.ktab = ktab; g.ntab = ntab; g.part = ws;                                \
-    g.rlo = rlo; g.rhi = rhi;                                                                                \
+    g.rlo = rlo; g.rhi = rhi; g.clo = clo; g.chi = chi;                                                      \
     g.rb = 2;                                                                                                \
     while (g.rb < kRB && (long long)B * g.nstrips * div_up(rhi - rlo, g.rb * 2) >= target_waves()) g.rb *= 2; \
     g.ntr = std::max(div_up(rhi - rlo, g.rb), 1);                                                            \

@@ -1,30 +1,36 @@
-"""Domain-decomposed V-cycle over several MI355X GPUs: row slabs + halo exchange.
+"""Domain-decomposed V-cycle over several MI355X GPUs: 2-D blocks + halo exchange.
 
-The fine grid ((m+1) x (n+1) nodes, Poisson) is cut into P row slabs, one per rank (one process
-per GPU, torch.distributed over RCCL/xGMI).  Levels 0 .. Ld-1 are distributed; the level-Ld
-restriction is all-gathered and the rest of the V-cycle (levels >= Ld of the global grid) is solved
-redundantly on every rank by a single-GPU MultigridSolver, whose correction each rank copies back
-for its slab.  The result is bitwise the single-GPU V-cycle on the global grid (same kernels, same
-per-node arithmetic, same coarse schedule), which the tests check.
+The fine grid ((m+1) x (n+1) nodes, Poisson) is cut into a Pr x Pc grid of blocks, one per rank (one
+process per GPU, torch.distributed over RCCL/xGMI; rank r = ri * Pc + ci).  Row slabs are the Pc = 1
+case.  Levels 0 .. Ld-1 are distributed; the level-Ld restriction is all-gathered and the rest of the
+V-cycle (levels >= Ld of the global grid) is solved redundantly on every rank by a single-GPU
+MultigridSolver, whose correction each rank copies back for its block.  The result is bitwise the
+single-GPU V-cycle on the global grid (same kernels, same per-node arithmetic, same coarse schedule),
+which the tests check.
 
-Layout (class Partition).  Interior row offsets t_r = r * m / P split level 0; level l uses
-t_r / 2^l, so fine rows (2I-1, 2I) and coarse row I always live on the same rank.  Rank r owns
-global rows [s, e) = [1 + t_r, 1 + t_{r+1}) (the last rank up to H-1) and stores rows
-[gr0, gr0 + Hloc) with gr0 = t_r - G_l (0 on rank 0): G_l = G * 2^(Ld-l) ghost rows per side, the
-doubling keeping gr0_l = 2 gr0_{l+1} so the unmodified level kernels pair fine and coarse rows
-exactly as on one grid.  The level kernels compute every local interior row; ghost rows near the
-slab edge are refreshed by exchanges, deeper ones are redundant work (G_0 rows per side, a few %).
+Layout (class Partition, one per axis).  Interior row offsets t_r = r * m / Pr split level 0; level l
+uses t_r / 2^l, so fine rows (2I-1, 2I) and coarse row I always live on the same rank.  Rank row ri
+owns global rows [s, e) = [1 + t_ri, 1 + t_ri+1) (the last one up to H-1) and stores rows
+[gr0, gr0 + Hloc) with gr0 = t_ri - G_l (0 on the first): G_l = G * 2^(Ld-l) ghost rows per side, the
+doubling keeping gr0_l = 2 gr0_{l+1} so the unmodified level kernels pair fine and coarse rows exactly
+as on one grid.  Columns are split the same way (same G).  The level kernels compute every local
+interior node (a block is just a smaller rectangular grid to them); ghost rows and columns near the
+block edge are refreshed by exchanges, deeper ones are redundant work.
 
-Communication (communication-avoiding).  Every level kernel already computes the ghost rows it
-stores, so ghost rows stay correct to a depth that shrinks by one row per sweep and halves per
-restriction; an exchange is needed only where that depth would run out.  Per V-cycle:
-  after the finest pre-smoothing (or the cycle join):  D1 rows of f_1 (and D0 rows of the
-                                                       pre-smoothed finest iterate, joined cycles)
-  at level Ld:  all-gather of the owned rows of f_Ld -> the replicated coarse solve -> local copy
-  after the finest post-smoothing (unjoined cycles):   D0 rows of the finest iterate
-i.e. ONE batch of neighbour messages and one all-gather per V-cycle, whatever Ld.  D0 and D1 are the
-smallest depths for which a row-validity simulation of the schedule (exchange_depths) keeps every
-owned row exact; the result stays bitwise the single-GPU V-cycle.
+Communication (communication-avoiding).  Every level kernel already computes the ghost nodes it
+stores, so ghost values stay correct to a depth that shrinks by one per sweep and halves per
+restriction — the same in both directions, so one scalar depth describes a block's valid region and
+the validity simulation of the slab case (exchange_depths) applies unchanged; an exchange is needed
+only where that depth would run out.  Per V-cycle:
+  after the finest pre-smoothing (or the cycle join):  D1 of f_1 (and D0 of the pre-smoothed finest
+                                                       iterate, joined cycles)
+  at level Ld:  all-gather of the owned blocks of f_Ld -> the replicated coarse solve -> local copy
+  after the finest post-smoothing (unjoined cycles):   D0 of the finest iterate
+An exchange of depth d runs in two phases: x (left/right neighbours: d ghost COLUMNS of the owned rows,
+packed strips) then y (up/down neighbours: d ghost ROWS over the whole local width, contiguous runs of
+the framed layout that now include the ghost columns just received), so the corner regions the
+9-point stencil needs arrive from the diagonal neighbours without corner messages.  D0 and D1 are the
+smallest depths for which the validity simulation keeps every owned node exact.
 """
 import torch
 
@@ -42,11 +48,12 @@ def global_levels(m, n):
     return L
 
 
-def default_agglomeration(m, n, P, L, max_nodes=1 << 20):
-    """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows."""
+def default_agglomeration(m, n, P, L, max_nodes=1 << 20, Pc=1):
+    """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows (P row
+    blocks, Pc column blocks)."""
     Ld = 1
     while Ld < L - 1 and ((m >> Ld) + 1) * ((n >> Ld) + 1) > max_nodes and m % (P << (Ld + 1)) == 0 \
-            and m // (P << (Ld + 1)) >= 4:
+            and m // (P << (Ld + 1)) >= 4 and n % (Pc << (Ld + 1)) == 0 and (Pc == 1 or n // (Pc << (Ld + 1)) >= 4):
         Ld += 1
     return Ld
 
@@ -65,6 +72,10 @@ class LevelPart:
 
 
 class Partition:
+    """One axis of the decomposition: m intervals split over P ranks for Ld distributed levels with G
+    ghost lines per side at level Ld (doubling per finer level); n: the other axis' intervals (checked
+    to coarsen Ld times).  Rows of the slab layout; the column axis of a 2-D grid is Partition(n, m, Pc)."""
+
     def __init__(self, m, n, P, Ld, G=4):
         if P < 1 or Ld < 1:
             raise ValueError("Partition: need P >= 1 and Ld >= 1")
@@ -91,6 +102,46 @@ class Partition:
         gr0 = 0 if r == 0 else t - g
         gend = H if r == self.P - 1 else e + g
         return LevelPart(H, s, e, gr0, gend)
+
+
+class Partition2D:
+    """Pr x Pc blocks (rank r = ri * Pc + ci): a row Partition and a column Partition with the same G and
+    Ld.  level(l, r) / clevel(l, r): rank r's row / column LevelPart of level l."""
+
+    def __init__(self, m, n, Pr, Pc, Ld, G=4):
+        self.rows = Partition(m, n, Pr, Ld, G)
+        self.cols = Partition(n, m, Pc, Ld, G) if Pc > 1 else None
+        self.m, self.n, self.Pr, self.Pc, self.Ld, self.G = m, n, Pr, Pc, Ld, G
+        self.P = Pr * Pc
+
+    def ghost(self, l):
+        return self.rows.ghost(l)
+
+    def rows_per_rank(self, l):
+        return self.rows.rows_per_rank(l)
+
+    def cols_per_rank(self, l):
+        return (self.n // self.Pc) >> l
+
+    def level(self, l, r):
+        return self.rows.level(l, r // self.Pc)
+
+    def clevel(self, l, r):
+        if self.cols is None:  # one column block: all columns, no ghosts
+            W = (self.n >> l) + 1
+            return LevelPart(W, 1, W - 1, 0, W)
+        return self.cols.level(l, r % self.Pc)
+
+
+def default_grid(P):
+    """Pr x Pc for P ranks: rows split at least as finely as columns (a row halo is one contiguous run
+    of the framed layout, a column halo a packed strip), as square as possible: 2 -> 2x1, 4 -> 2x2,
+    8 -> 4x2."""
+    best = (P, 1)
+    for Pc in range(1, P + 1):
+        if P % Pc == 0 and P // Pc >= Pc:
+            best = (P // Pc, Pc)
+    return best
 
 
 def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a", depths=(4, 4)):
@@ -258,13 +309,17 @@ def _joined(nu1, nu2, fuse):
     return nu1 == 1 and nu2 == 1 and fuse
 
 
-def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True):
-    """The slab partition with the fewest ghost rows (G ghost rows at level Ld, doubling per finer
-    level) for which exchange depths exist, and those depths.  Ghost rows are redundant work."""
+def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None):
+    """The Pr x Pc partition (default P x 1: row slabs) with the fewest ghost lines (G at level Ld,
+    doubling per finer level) for which exchange depths exist, and those depths.  Ghost lines are
+    redundant work."""
+    Pr, Pc = grid if grid is not None else (P, 1)
+    if Pr * Pc != P:
+        raise ValueError(f"DD: grid {Pr} x {Pc} does not hold {P} ranks")
     err = None
     for G in (2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
         try:
-            part = Partition(m, n, P, Ld, G)
+            part = Partition2D(m, n, Pr, Pc, Ld, G)
         except ValueError as e:
             err = e
             break
@@ -272,7 +327,7 @@ def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True):
             return part, exchange_depths(Ld, part.ghost, nu1, nu2, fuse, joined=_joined(nu1, nu2, fuse))
         except ValueError as e:
             err = e
-    raise ValueError(f"DD: no slab partition of {m} rows over {P} ranks with Ld = {Ld}: {err}")
+    raise ValueError(f"DD: no {Pr} x {Pc} partition of a {m} x {n} grid with Ld = {Ld}: {err}")
 
 
 def _launch_list(launches, dtype, stream):
@@ -290,37 +345,50 @@ def _rows(t, B, bs, ld, y0, y1):
     return t.as_strided((B, (y1 - y0) * ld), (bs, 1), t.storage_offset() + (y0 + 1) * ld)
 
 
+def _block(t, B, bs, ld, y0, y1, x0, x1):
+    """[B, y1-y0, x1-x0] (strided) view of local rows y0..y1-1, columns x0..x1-1 of a framed buffer."""
+    off = 128 // t.element_size() - 1
+    return t.as_strided((B, y1 - y0, x1 - x0), (bs, ld, 1), t.storage_offset() + (y0 + 1) * ld + off + x0)
+
+
 class DDSolver:
     """One rank of the domain-decomposed V-cycle.
 
     Args: n, rows: global intervals (columns, rows) of the fine grid; rank, world: this rank and the
-    number of slabs; comm: a TorchComm (one process per GPU) or None when driven by a LocalGroup;
-    agglomerate: Ld (default: see default_agglomeration); other args as MultigridSolver (Poisson).
+    number of ranks; grid: (Pr, Pc) blocks, Pr * Pc = world (default (world, 1): row slabs; see
+    default_grid for the 2-D choice); comm: a TorchComm (one process per GPU) or None when driven by a
+    LocalGroup; agglomerate: Ld (default: see default_agglomeration); other args as MultigridSolver
+    (Poisson).
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
-                 batch=1, nu1=1, nu2=1, fuse=True, graph=True):
+                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None):
         self.n, self.m = n, rows
         self.rank, self.P = rank, world
+        self.Pr, self.Pc = grid if grid is not None else (world, 1)
+        self.ri, self.ci = divmod(rank, self.Pc)
         self.comm = comm
         self.L = global_levels(rows, n)
-        self.Ld = default_agglomeration(rows, n, world, self.L) if agglomerate is None else int(agglomerate)
+        self.Ld = (default_agglomeration(rows, n, self.Pr, self.L, Pc=self.Pc) if agglomerate is None
+                   else int(agglomerate))
         if not 1 <= self.Ld <= self.L - 1:
             raise ValueError(f"DDSolver: agglomeration level {self.Ld} outside [1, {self.L - 1}]")
-        self.part, self.depths = _partition_for(rows, n, world, self.Ld, nu1, nu2, fuse)
-        self.parts = [self.part.level(l, rank) for l in range(self.Ld + 1)]
+        self.part, self.depths = _partition_for(rows, n, world, self.Ld, nu1, nu2, fuse, grid=(self.Pr, self.Pc))
+        self.parts = [self.part.level(l, rank) for l in range(self.Ld + 1)]    # rows
+        self.cparts = [self.part.clevel(l, rank) for l in range(self.Ld + 1)]  # columns
         self.dtype, self.B = dtype, batch
         self.device = torch.device(device if device is not None else "cuda")
         self.nu1, self.nu2, self.fuse = nu1, nu2, fuse
-        p0 = self.parts[0]
-        self.local = MultigridSolver(n, rows=p0.Hloc - 1, levels=self.Ld + 1, dtype=dtype, device=self.device,
-                                     batch=batch, nu1=nu1, nu2=nu2, fuse=fuse, coarse_tail=False, graph=False)
+        p0, q0 = self.parts[0], self.cparts[0]
+        self.local = MultigridSolver(q0.Hloc - 1, rows=p0.Hloc - 1, levels=self.Ld + 1, dtype=dtype,
+                                     device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse, coarse_tail=False,
+                                     graph=False)
         self.coarse = MultigridSolver(n >> self.Ld, rows=rows >> self.Ld, levels=self.L - self.Ld, dtype=dtype,
                                       device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse,
                                       coarse_tail=True, graph=False, zero_start=True)
-        for l, lp in enumerate(self.parts):
+        for l, (lp, lq) in enumerate(zip(self.parts, self.cparts)):
             Lv = self.local.levels[l]
-            assert Lv.H == lp.Hloc and Lv.W == (n >> l) + 1, (l, Lv.H, lp)
+            assert Lv.H == lp.Hloc and Lv.W == lq.Hloc, (l, Lv.H, Lv.W, lp, lq)
         self.coarse_plan, self.coarse_end = self.coarse._build("a")
         assert self.joinable() == _joined(nu1, nu2, fuse)
         self.use_graph = graph
@@ -339,12 +407,13 @@ class DDSolver:
         return self.n + 1
 
     def _local_rows(self, x):
-        """Rows [gr0, gr0 + Hloc) of a global [B, 1, H, W] tensor, contiguous."""
-        p0 = self.parts[0]
+        """This rank's stored block (rows [gr0, gr0 + Hloc), columns [gc0, gc0 + Wloc)) of a global
+        [B, 1, H, W] tensor, contiguous."""
+        p0, q0 = self.parts[0], self.cparts[0]
         x = x.to(self.device, self.dtype).reshape(-1, 1, self.H, self.W)
         if x.shape[0] == 1 and self.B > 1:
             x = x.expand(self.B, 1, self.H, self.W)
-        return x[:, :, p0.gr0:p0.gr0 + p0.Hloc].contiguous()
+        return x[:, :, p0.gr0:p0.gr0 + p0.Hloc, q0.gr0:q0.gr0 + q0.Hloc].contiguous()
 
     def set_rhs(self, f):
         """Assembled right-hand side of the GLOBAL problem, [B, 1, H, W] (any device)."""
@@ -365,21 +434,37 @@ class DDSolver:
         self.local._pack(x, L0.b, reset=False)
         self._state = "a"
 
+    def owned_block(self):
+        """((y0, y1), (x0, x1), u[B, 1, y1-y0, x1-x0]): the current iterate on the global nodes this rank
+        owns — its interior block plus the global boundary lines on the edges of the domain it touches,
+        so the ranks' blocks tile the whole grid."""
+        p0, q0 = self.parts[0], self.cparts[0]
+        L0 = self.local.levels[0]
+        v = L0.view(L0.buf(self._state))
+        ly0 = 0 if self.ri == 0 else p0.lo
+        ly1 = p0.Hloc if self.ri == self.Pr - 1 else p0.hi
+        lx0 = 0 if self.ci == 0 else q0.lo
+        lx1 = q0.Hloc if self.ci == self.Pc - 1 else q0.hi
+        return ((p0.gr0 + ly0, p0.gr0 + ly1), (q0.gr0 + lx0, q0.gr0 + lx1),
+                v[:, ly0:ly1, lx0:lx1].unsqueeze(1).clone())
+
     def owned_solution(self):
-        """(s, e, u[B, 1, e-s, W]): the current iterate on the rows this rank owns."""
+        """(s, e, u[B, 1, e-s, W]): the current iterate on the interior rows this rank owns (row slabs)."""
+        if self.Pc != 1:
+            raise RuntimeError("DDSolver.owned_solution: row slabs only; use owned_block()")
         p0 = self.parts[0]
         L0 = self.local.levels[0]
         v = L0.view(L0.buf(self._state))
         return p0.s, p0.e, v[:, p0.lo:p0.hi].unsqueeze(1).clone()
 
     def residual_norm_sq_local(self):
-        """Sum over owned rows of (f - K u)^2 per sample (float64 device tensor [B])."""
+        """Sum over owned interior nodes of (f - K u)^2 per sample (float64 device tensor [B])."""
         L0 = self.local.levels[0]
-        p0 = self.parts[0]
+        p0, q0 = self.parts[0], self.cparts[0]
         loc = self.local
         _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(), None,
                   loc.ktab.data_ptr(), loc.ntab, loc.norm_out.data_ptr(), loc.ws.data_ptr(), *L0.geom(),
-                  p0.lo, p0.hi, torch.cuda.current_stream(self.device).cuda_stream)
+                  p0.lo, p0.hi, q0.lo, q0.hi, torch.cuda.current_stream(self.device).cuda_stream)
         return loc.norm_out * loc.norm_out
 
     # ------------------------------------------------------------------ plan
@@ -405,10 +490,7 @@ class DDSolver:
             if st[0] == "gather":  # one rank: the all-gather is a device copy
                 launches = [("copy", (self.gather_target(), self.gather_source()))]
             elif st[0] == "scatter":  # a device copy, captured with the kernels around it
-                pl = self.parts[self.Ld]
-                Lc = self.coarse.levels[0]
-                src = _rows(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc)
-                launches = [("copy", (self.level_rows(self.Ld, st[1], 0, pl.Hloc), src))]
+                launches = [("copy", self.scatter_views(st[1]))]
             elif st[0] == "coarse":
                 launches = list(self.coarse_plan)
             elif st[0] == "join":
@@ -497,24 +579,87 @@ class DDSolver:
         Lv = self.local.levels[l]
         return _rows(Lv.buf(name), Lv.B, Lv.bs, Lv.ld, y0, y1)
 
+    def level_block(self, l, name, y0, y1, x0, x1):
+        Lv = self.local.levels[l]
+        return _block(Lv.buf(name), Lv.B, Lv.bs, Lv.ld, y0, y1, x0, x1)
+
     def gather_source(self):
-        """Owned rows of f_Ld, padded to rows_per_rank (the last rank adds the zero boundary row)."""
-        pl = self.parts[self.Ld]
+        """Owned block of f_Ld padded to rows_per_rank x cols_per_rank (ranks on the last row / column
+        add the zero boundary line).  Row slabs: whole framed rows (a contiguous run)."""
+        pl, ql = self.parts[self.Ld], self.cparts[self.Ld]
         c = self.part.rows_per_rank(self.Ld)
-        return self.level_rows(self.Ld, "f", pl.lo, pl.lo + c)
+        if self.Pc == 1:
+            return self.level_rows(self.Ld, "f", pl.lo, pl.lo + c)
+        return self.level_block(self.Ld, "f", pl.lo, pl.lo + c, ql.lo, ql.lo + self.part.cols_per_rank(self.Ld))
 
     def gather_target(self):
-        """Rows [1, 1 + P*c) of the coarse solver's top-level f: the P gathered chunks in rank order."""
+        """Row slabs: rows [1, 1 + P*c) of the coarse solver's top-level f (the P chunks in rank order).
+        2-D blocks: a [P, B, c_r, c_c] staging buffer, placed by gather_place()."""
         Lc = self.coarse.levels[0]
         c = self.part.rows_per_rank(self.Ld)
-        return _rows(Lc.f, Lc.B, Lc.bs, Lc.ld, 1, 1 + self.P * c)
+        if self.Pc == 1:
+            return _rows(Lc.f, Lc.B, Lc.bs, Lc.ld, 1, 1 + self.P * c)
+        if getattr(self, "_gstage", None) is None:
+            cc = self.part.cols_per_rank(self.Ld)
+            self._gstage = torch.empty((self.P, self.B, c, cc), dtype=self.dtype, device=self.device)
+            self._gsend = torch.empty((self.B, c, cc), dtype=self.dtype, device=self.device)
+        return self._gstage
+
+    def gather_place(self, blocks):
+        """2-D blocks: copy the gathered blocks ([P, B, c_r, c_c], rank order) into the coarse f."""
+        Lc = self.coarse.levels[0]
+        c, cc = self.part.rows_per_rank(self.Ld), self.part.cols_per_rank(self.Ld)
+        for q in range(self.P):
+            qi, qj = divmod(q, self.Pc)
+            _block(Lc.f, Lc.B, Lc.bs, Lc.ld, 1 + qi * c, 1 + (qi + 1) * c, 1 + qj * cc, 1 + (qj + 1) * cc).copy_(blocks[q])
+
+    def gather(self):
+        """The level-Ld all-gather over the communicator (the coarse solver's f on every rank)."""
+        if self.Pc == 1:
+            self.comm.allgather(self.gather_target(), self.gather_source())
+            return
+        tgt = self.gather_target()
+        self._gsend.copy_(self.gather_source())
+        self.comm.allgather(tgt, self._gsend)
+        self.gather_place(tgt)
+
+    def scatter_views(self, dst):
+        """(destination, source): this rank's stored block of the coarse solution -> level Ld's `dst`."""
+        pl, ql = self.parts[self.Ld], self.cparts[self.Ld]
+        Lc = self.coarse.levels[0]
+        if self.Pc == 1:
+            src = _rows(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc)
+            return self.level_rows(self.Ld, dst, 0, pl.Hloc), src
+        src = _block(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc, ql.gr0, ql.gr0 + ql.Hloc)
+        return self.level_block(self.Ld, dst, 0, pl.Hloc, 0, ql.Hloc), src
 
     def scatter(self, dst):
-        """Copy this rank's rows of the coarse solution into level Ld's buffer `dst`."""
-        pl = self.parts[self.Ld]
-        Lc = self.coarse.levels[0]
-        src = _rows(Lc.buf(self.coarse_end), Lc.B, Lc.bs, Lc.ld, pl.gr0, pl.gr0 + pl.Hloc)
-        self.level_rows(self.Ld, dst, 0, pl.Hloc).copy_(src)
+        """Copy this rank's block of the coarse solution into level Ld's buffer `dst`."""
+        d, s = self.scatter_views(dst)
+        d.copy_(s)
+
+    def halo(self, l, name, d, phase):
+        """Halo transfers of one exchange phase on level l's buffer `name`, depth d:
+        [(send view, peer rank, receive view)].  x: d ghost columns of the owned rows to/from the left
+        and right neighbours; y: d ghost rows over the whole local width (ghost columns included) to/from
+        the neighbours above and below."""
+        lp, lq = self.parts[l], self.cparts[l]
+        out = []
+        if phase == "x":
+            if self.ci > 0:
+                out.append((self.level_block(l, name, lp.lo, lp.hi, lq.lo, lq.lo + d), self.rank - 1,
+                            self.level_block(l, name, lp.lo, lp.hi, lq.lo - d, lq.lo)))
+            if self.ci < self.Pc - 1:
+                out.append((self.level_block(l, name, lp.lo, lp.hi, lq.hi - d, lq.hi), self.rank + 1,
+                            self.level_block(l, name, lp.lo, lp.hi, lq.hi, lq.hi + d)))
+        else:
+            if self.ri > 0:
+                out.append((self.level_rows(l, name, lp.lo, lp.lo + d), self.rank - self.Pc,
+                            self.level_rows(l, name, lp.lo - d, lp.lo)))
+            if self.ri < self.Pr - 1:
+                out.append((self.level_rows(l, name, lp.hi - d, lp.hi), self.rank + self.Pc,
+                            self.level_rows(l, name, lp.hi, lp.hi + d)))
+        return out
 
     # ------------------------------------------------------------------ driver (one process per rank)
     def vcycle(self, k=1):
@@ -545,7 +690,7 @@ class DDSolver:
                     if later:
                         pending = self.comm.exchange_many(self, later, wait=False)
                 elif st[0] == "gather":
-                    self.comm.allgather(self.gather_target(), self.gather_source())
+                    self.gather()
                 elif st[0] == "scatter":
                     self.scatter(st[1])
         if pending is not None:
@@ -586,51 +731,51 @@ class TorchComm:
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])
 
+    def _phase_plan(self, s, items, phase):
+        """P2P ops of one exchange phase for every (level, buffer, d) in `items` (DDSolver.halo), with
+        send/receive buffers: the views themselves when they are contiguous device rows (RCCL), else
+        staging buffers (packed column strips; host memory for gloo)."""
+        dist = self.dist
+        trans = [t for l, name, d in items for t in s.halo(l, name, d, phase)]
+        direct = self.gpu and all(a.is_contiguous() and b.is_contiguous() for a, _, b in trans)
+        if direct:
+            sb = [a for a, _, _ in trans]
+            rb = [b for _, _, b in trans]
+        else:
+            dev = trans[0][0].device if (trans and self.gpu) else "cpu"
+            sb = [torch.empty(a.shape, dtype=a.dtype, device=dev) for a, _, _ in trans]
+            rb = [torch.empty(b.shape, dtype=b.dtype, device=dev) for _, _, b in trans]
+        ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, (_, peer, _) in zip(sb, trans)]
+        ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, (_, peer, _) in zip(rb, trans)]
+        return (ops, direct, list(zip(sb, [a for a, _, _ in trans])), list(zip(rb, [b for _, _, b in trans])))
+
     def exchange_many(self, s, items, wait=True):
-        """Refresh d ghost rows on both sides of rank s's slab for every (level, buffer, d) in `items`,
-        as ONE batch of P2P ops.  The op lists are built once per item list and reused (fixed device
-        views).  wait=False: return a handle for exchange_finish instead of completing the batch (with
-        RCCL the ops run on the communicator's stream meanwhile; finishing makes the current stream
-        wait for them, the host does not block)."""
+        """Refresh d ghost lines around rank s's block for every (level, buffer, d) in `items`: the x phase
+        (ghost columns, left/right neighbours) as ONE batch of P2P ops, completed, then the y phase (ghost
+        rows incl. the new ghost columns, up/down) as one batch.  The op lists are built once per item
+        list and reused (fixed device views).  wait=False: return a handle for exchange_finish instead
+        of completing the last batch (with RCCL its ops run on the communicator's stream meanwhile;
+        finishing makes the current stream wait for them, the host does not block)."""
         dist = self.dist
         # plans hold views of s's buffers: cached on s itself (keyed by this communicator), never on
         # the communicator under id(s), which a later solver could reuse
         plans = s.__dict__.setdefault("_comm_plans", {})
         key = (id(self), tuple(items))
-        plan = plans.get(key)
-        if plan is None:
-            sends, recvs = [], []
-            for l, name, d in items:
-                lp = s.parts[l]
-                if s.rank > 0:
-                    sends.append((s.level_rows(l, name, lp.lo, lp.lo + d), s.rank - 1))
-                    recvs.append((s.level_rows(l, name, lp.lo - d, lp.lo), s.rank - 1))
-                if s.rank < s.P - 1:
-                    sends.append((s.level_rows(l, name, lp.hi - d, lp.hi), s.rank + 1))
-                    recvs.append((s.level_rows(l, name, lp.hi, lp.hi + d), s.rank + 1))
-            direct = self.gpu and all(t.is_contiguous() for t, _ in sends + recvs)
-            if direct:
-                sb = [t for t, _ in sends]
-                rb = [t for t, _ in recvs]
-            else:
-                dev = sends[0][0].device if (sends and self.gpu) else "cpu"
-                sb = [torch.empty(t.shape, dtype=t.dtype, device=dev) for t, _ in sends]
-                rb = [torch.empty(t.shape, dtype=t.dtype, device=dev) for t, _ in recvs]
-            ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, (_, peer) in zip(sb, sends)]
-            ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, (_, peer) in zip(rb, recvs)]
-            plan = (ops, direct, list(zip(sb, [t for t, _ in sends])), list(zip(rb, [t for t, _ in recvs])))
-            plans[key] = plan
-        ops, direct, spairs, rpairs = plan
-        if not ops:
-            return None
-        if not direct:
-            for b, t in spairs:
-                b.copy_(t)
-        handle = (dist.batch_isend_irecv(ops), direct, rpairs)
-        if not wait:
-            return handle
-        self.exchange_finish(handle)
-        return None
+        phases = plans.get(key)
+        if phases is None:
+            phases = [self._phase_plan(s, items, ph) for ph, n in (("x", s.Pc), ("y", s.Pr)) if n > 1]
+            phases = [p for p in phases if p[0]]
+            plans[key] = phases
+        handle = None
+        for i, (ops, direct, spairs, rpairs) in enumerate(phases):
+            if not direct:
+                for b, t in spairs:
+                    b.copy_(t)
+            handle = (dist.batch_isend_irecv(ops), direct, rpairs)
+            if wait or i < len(phases) - 1:
+                self.exchange_finish(handle)
+                handle = None
+        return handle
 
     def exchange_finish(self, handle):
         if handle is None:
@@ -650,6 +795,9 @@ class TorchComm:
         src = self._stage(source)
         parts = [torch.empty_like(src) for _ in range(self.world)]
         dist.all_gather(parts, src, group=self.group)
+        if target.dim() == 4:  # 2-D blocks: [P, B, c_r, c_c] staging, rank order
+            target.copy_(torch.stack(parts, 0))
+            return
         B = source.shape[0]
         full = torch.stack([p.reshape(B, -1) for p in parts], 1).reshape(B, -1)
         target.copy_(full)
@@ -668,7 +816,7 @@ class LocalGroup:
     exchanges done as device copies.  Used to test the decomposition on a single GPU."""
 
     def __init__(self, n, rows, world, **kw):
-        self.ranks = [DDSolver(n, rows, r, world, comm=None, **kw) for r in range(world)]
+        self.ranks = [DDSolver(n, rows, r, world, comm=None, **kw) for r in range(world)]  # kw: grid=(Pr, Pc), ...
 
     def set_rhs(self, f):
         for s in self.ranks:
@@ -695,9 +843,14 @@ class LocalGroup:
                     chunks = [s.gather_source() for s in self.ranks]
                     for s in self.ranks:
                         tgt = s.gather_target()
-                        c = chunks[0].shape[1]
-                        for r, ch in enumerate(chunks):
-                            tgt[:, r * c:(r + 1) * c].copy_(ch)
+                        if s.Pc == 1:
+                            c = chunks[0].shape[1]
+                            for r, ch in enumerate(chunks):
+                                tgt[:, r * c:(r + 1) * c].copy_(ch)
+                        else:
+                            for r, ch in enumerate(chunks):
+                                tgt[r].copy_(ch)
+                            s.gather_place(tgt)
                 elif st[0] == "scatter":
                     for s in self.ranks:
                         s.scatter(st[1])
@@ -705,31 +858,23 @@ class LocalGroup:
             s._state = end
 
     def _exchange(self, l, name, d):
-        for r, s in enumerate(self.ranks):
-            lp = s.parts[l]
-            if r > 0:
-                q = self.ranks[r - 1]
-                qp = q.parts[l]
-                s.level_rows(l, name, lp.lo - d, lp.lo).copy_(q.level_rows(l, name, qp.hi - d, qp.hi))
-            if r < len(self.ranks) - 1:
-                q = self.ranks[r + 1]
-                qp = q.parts[l]
-                s.level_rows(l, name, lp.hi, lp.hi + d).copy_(q.level_rows(l, name, qp.lo, qp.lo + d))
+        """The two phases of TorchComm.exchange_many as device copies: every rank's x phase, then every
+        rank's y phase (which carries the ghost columns just received)."""
+        for phase in ("x", "y"):
+            for s in self.ranks:
+                for send, peer, _ in s.halo(l, name, d, phase):
+                    q = self.ranks[peer]
+                    # the peer's receive view that pairs with this send (the opposite side)
+                    recv = [rv for _, pr, rv in q.halo(l, name, d, phase) if pr == s.rank]
+                    recv[0].copy_(send)
 
     def solution(self):
-        """Global iterate assembled from the owned rows (boundary rows from ranks 0 / P-1)."""
+        """Global iterate assembled from the ranks' owned blocks (they tile the grid)."""
         s0 = self.ranks[0]
         out = torch.zeros((s0.B, 1, s0.H, s0.W), dtype=s0.dtype, device=s0.device)
         for s in self.ranks:
-            a, b, u = s.owned_solution()
-            out[:, :, a:b] = u
-            L0 = s.local.levels[0]
-            v = L0.view(L0.buf(s._state))
-            p0 = s.parts[0]
-            if s.rank == 0:
-                out[:, 0, 0] = v[:, 0]
-            if s.rank == s.P - 1:
-                out[:, 0, -1] = v[:, p0.Hloc - 1]
+            (y0, y1), (x0, x1), u = s.owned_block()
+            out[:, :, y0:y1, x0:x1] = u
         return out
 
     def residual_norm(self):

@@ -324,7 +324,7 @@ class MultigridSolver:
         L0 = self.levels[0]
         _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(),
                   None if L0.pid is None else L0.pid.data_ptr(), self.ktab.data_ptr(), self.ntab,
-                  self.norm_out.data_ptr(), self.ws.data_ptr(), *L0.geom(), 0, 0,
+                  self.norm_out.data_ptr(), self.ws.data_ptr(), *L0.geom(), 0, 0, 0, 0,
                   torch.cuda.current_stream(self.device).cuda_stream)
         return self.norm_out.clone()
 

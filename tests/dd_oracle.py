@@ -1,6 +1,7 @@
 """CPU restatement of one rank of the domain-decomposed V-cycle (feanet_amd.dd) with the oracle's
-operators on numpy slabs and torch.distributed (gloo) for the exchanges: checks the partition,
-the communication schedule and the coarse agglomeration without a GPU.  Test infrastructure."""
+operators on numpy blocks and torch.distributed (gloo) for the exchanges: checks the 2-D partition
+(row slabs = 1 column block), the two-phase halo exchange, the communication schedule and the coarse
+agglomeration without a GPU.  Test infrastructure."""
 import os
 import sys
 
@@ -23,27 +24,33 @@ def problem(m, n, B, seed=0):
 
 
 class OracleRank:
-    """Rank r's local levels as numpy arrays, kernel steps executed with oracle operators (local
-    boundary rows are kept, the framed kernels' semantics)."""
+    """Rank r's local levels as numpy arrays (its stored block: rows [gr0, gr0 + Hloc) x columns
+    [gc0, gc0 + Wloc)), kernel steps executed with oracle operators (the block's edge lines are kept,
+    the framed kernels' semantics)."""
 
-    def __init__(self, m, n, P, r, Ld, f, u, nu=(1, 1)):
+    def __init__(self, m, n, P, r, Ld, f, u, nu=(1, 1), grid=None):
         from feanet_amd.dd import _partition_for, global_levels
         self.m, self.n, self.P, self.r, self.Ld = m, n, P, r, Ld
+        self.Pr, self.Pc = grid if grid is not None else (P, 1)
+        self.ri, self.ci = divmod(r, self.Pc)
         self.L = global_levels(m, n)
         # the partition and exchange depths DDSolver uses (the oracle runs its unjoined cycles)
-        self.part, self.depths = _partition_for(m, n, P, Ld, nu[0], nu[1], fuse=True)
+        self.part, self.depths = _partition_for(m, n, P, Ld, nu[0], nu[1], fuse=True, grid=(self.Pr, self.Pc))
         self.parts = [self.part.level(l, r) for l in range(Ld + 1)]
-        self.lv = [orc.Level(n >> l, "poisson", np.float64, m=p.Hloc - 1) for l, p in enumerate(self.parts)]
+        self.cparts = [self.part.clevel(l, r) for l in range(Ld + 1)]
+        self.lv = [orc.Level(q.Hloc - 1, "poisson", np.float64, m=p.Hloc - 1)
+                   for p, q in zip(self.parts, self.cparts)]
         B = f.shape[0]
         self.B = B
-        p0 = self.parts[0]
+        p0, q0 = self.parts[0], self.cparts[0]
         self.bufs = [dict() for _ in range(Ld + 1)]
-        for l, p in enumerate(self.parts):
-            z = np.zeros((B, p.Hloc, (n >> l) + 1))
+        for l, (p, q) in enumerate(zip(self.parts, self.cparts)):
+            z = np.zeros((B, p.Hloc, q.Hloc))
             self.bufs[l] = {"f": z.copy(), "a": z.copy(), "b": z.copy(), "zero": z.copy()}
-        self.bufs[0]["f"] = f[:, p0.gr0:p0.gr0 + p0.Hloc].copy()
-        self.bufs[0]["a"] = u[:, p0.gr0:p0.gr0 + p0.Hloc].copy()
-        self.bufs[0]["b"] = u[:, p0.gr0:p0.gr0 + p0.Hloc].copy()
+        blk = (slice(None), slice(p0.gr0, p0.gr0 + p0.Hloc), slice(q0.gr0, q0.gr0 + q0.Hloc))
+        self.bufs[0]["f"] = f[blk].copy()
+        self.bufs[0]["a"] = u[blk].copy()
+        self.bufs[0]["b"] = u[blk].copy()
         self.R = (orc.np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float32) / 4)[None]
         self.nu = nu
         self.coarse = orc.OracleMultigrid(n >> Ld, "poisson", np.float64, levels=self.L - Ld, rows=m >> Ld)
@@ -75,8 +82,8 @@ class OracleRank:
             keep[:, 1:-1, 1:-1] = fc[:, 1:-1, 1:-1]
             b[l + 1]["f"] = keep
         elif kind == "prolong_sweep":
-            # the kernel's semantics: the corrected field x enters the stencil on every row (also the
-            # slab's local edge rows), interior nodes are swept, edge rows keep the source values
+            # the kernel's semantics: the corrected field x enters the stencil on every node (also the
+            # block's local edge lines), interior nodes are swept, edge lines keep the source values
             src = self.sweep(l, b[l]["zero"], b[l]["f"]) if st[2] == "omdf" else b[l][st[2]]
             x = src + orc.prolong(b[l + 1][st[3]], lv[l + 1].pid, self.R)
             omd = orc.omega_over_d(lv[l].ktab, 2. / 3., np.float64)[0]
@@ -85,8 +92,24 @@ class OracleRank:
         else:
             raise AssertionError(kind)
 
-    def rows(self, l, name, y0, y1):
-        return self.bufs[l][name][:, y0:y1]
+    def halo(self, l, name, d, phase):
+        """[(send array, peer, (row slice, column slice) to receive into)] — DDSolver.halo's regions."""
+        p, q = self.parts[l], self.cparts[l]
+        a = self.bufs[l][name]
+        out = []
+        if phase == "x":
+            rows = slice(p.lo, p.hi)
+            if self.ci > 0:
+                out.append((a[:, rows, q.lo:q.lo + d].copy(), self.r - 1, (rows, slice(q.lo - d, q.lo))))
+            if self.ci < self.Pc - 1:
+                out.append((a[:, rows, q.hi - d:q.hi].copy(), self.r + 1, (rows, slice(q.hi, q.hi + d))))
+        else:
+            cols = slice(None)
+            if self.ri > 0:
+                out.append((a[:, p.lo:p.lo + d].copy(), self.r - self.Pc, (slice(p.lo - d, p.lo), cols)))
+            if self.ri < self.Pr - 1:
+                out.append((a[:, p.hi - d:p.hi].copy(), self.r + self.Pc, (slice(p.hi, p.hi + d), cols)))
+        return out
 
     def coarse_solve(self, fglob):
         """The replicated coarse sub-cycle: the oracle V-cycle of levels >= Ld from a zero guess."""
@@ -99,55 +122,54 @@ class OracleRank:
         return bufs[0][end]
 
 
-def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2):
-    """Process entry: one rank of the oracle DD V-cycle over gloo; saves its owned rows."""
+def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2, grid=None):
+    """Process entry: one rank of the oracle DD V-cycle over gloo; saves its owned block."""
     import torch
     import torch.distributed as dist
     from feanet_amd.dd import dd_schedule
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     B = 2
     f, u = problem(m, n, B)
-    R = OracleRank(m, n, world, rank, Ld, f, u)
+    R = OracleRank(m, n, world, rank, Ld, f, u, grid=grid)
     state = "a"
     for _ in range(cycles):
         steps, end = dd_schedule(Ld, 1, 1, True, state, R.depths)
         for st in steps:
             if st[0] == "exchange":
                 l, name, DEPTH = st[1], st[2], st[3]
-                lp = R.parts[l]
-                ops, recv = [], []
-                if rank > 0:
-                    ops.append(dist.P2POp(dist.isend, torch.from_numpy(R.rows(l, name, lp.lo, lp.lo + DEPTH).copy()),
-                                          rank - 1))
-                    t = torch.empty((B, DEPTH, (n >> l) + 1), dtype=torch.float64)
-                    ops.append(dist.P2POp(dist.irecv, t, rank - 1))
-                    recv.append((t, lp.lo - DEPTH))
-                if rank < world - 1:
-                    ops.append(dist.P2POp(dist.isend, torch.from_numpy(R.rows(l, name, lp.hi - DEPTH, lp.hi).copy()),
-                                          rank + 1))
-                    t = torch.empty((B, DEPTH, (n >> l) + 1), dtype=torch.float64)
-                    ops.append(dist.P2POp(dist.irecv, t, rank + 1))
-                    recv.append((t, lp.hi))
-                for w in dist.batch_isend_irecv(ops):
-                    w.wait()
-                for t, y0 in recv:
-                    R.bufs[l][name][:, y0:y0 + DEPTH] = t.numpy()
+                for phase, cnt in (("x", R.Pc), ("y", R.Pr)):
+                    if cnt == 1:
+                        continue
+                    ops, recv = [], []
+                    for arr, peer, where in R.halo(l, name, DEPTH, phase):
+                        ops.append(dist.P2POp(dist.isend, torch.from_numpy(arr), peer))
+                        t = torch.empty(arr.shape, dtype=torch.float64)
+                        ops.append(dist.P2POp(dist.irecv, t, peer))
+                        recv.append((t, where))
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+                    for t, (rs, cs) in recv:
+                        R.bufs[l][name][:, rs, cs] = t.numpy()
             elif st[0] == "gather":
-                pl = R.parts[Ld]
-                c = R.part.rows_per_rank(Ld)
-                chunk = torch.from_numpy(R.rows(Ld, "f", pl.lo, pl.lo + c).copy())
+                pl, ql = R.parts[Ld], R.cparts[Ld]
+                c, cc = R.part.rows_per_rank(Ld), R.part.cols_per_rank(Ld)
+                chunk = torch.from_numpy(R.bufs[Ld]["f"][:, pl.lo:pl.lo + c, ql.lo:ql.lo + cc].copy())
                 parts = [torch.empty_like(chunk) for _ in range(world)]
                 dist.all_gather(parts, chunk)
                 fglob = np.zeros((B, (m >> Ld) + 1, (n >> Ld) + 1))
-                fglob[:, 1:1 + world * c] = np.concatenate([p.numpy() for p in parts], axis=1)
+                for q, pt in enumerate(parts):
+                    qi, qj = divmod(q, R.Pc)
+                    fglob[:, 1 + qi * c:1 + (qi + 1) * c, 1 + qj * cc:1 + (qj + 1) * cc] = pt.numpy()
             elif st[0] == "coarse":
                 eglob = R.coarse_solve(fglob)
             elif st[0] == "scatter":
-                pl = R.parts[Ld]
-                R.bufs[Ld][st[1]] = eglob[:, pl.gr0:pl.gr0 + pl.Hloc].copy()
+                pl, ql = R.parts[Ld], R.cparts[Ld]
+                R.bufs[Ld][st[1]] = eglob[:, pl.gr0:pl.gr0 + pl.Hloc, ql.gr0:ql.gr0 + ql.Hloc].copy()
             else:
                 R.kernel(st)
         state = end
-    p0 = R.parts[0]
-    np.save(os.path.join(outdir, f"rank{rank}.npy"), R.bufs[0][state][:, p0.lo:p0.hi])
+    p0, q0 = R.parts[0], R.cparts[0]
+    np.save(os.path.join(outdir, f"rank{rank}.npy"), R.bufs[0][state][:, p0.lo:p0.hi, q0.lo:q0.hi])
+    with open(os.path.join(outdir, f"rank{rank}.idx"), "w") as fh:
+        fh.write(f"{p0.s} {p0.e} {q0.s} {q0.e}\n")
     dist.destroy_process_group()

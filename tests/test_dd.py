@@ -9,7 +9,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from feanet_amd.dd import (Partition, _joined_chunk_steps, _partition_for, dd_schedule, default_agglomeration,
-                           exchange_depths, global_levels, simulate_validity)
+                           exchange_depths, global_levels, simulate_validity)  # noqa: F401
 from oracle import feanet_oracle as orc
 
 
@@ -108,16 +108,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, m, n, Ld, port, outdir):
+def _worker(rank, world, m, n, Ld, port, outdir, grid):
     import dd_oracle
-    dd_oracle.run_rank(rank, world, m, n, Ld, port, outdir)
+    dd_oracle.run_rank(rank, world, m, n, Ld, port, outdir, grid=grid)
 
 
-@pytest.mark.parametrize("m,n,P,Ld", [(64, 32, 2, 2), (96, 32, 3, 2), (128, 64, 2, 3)])
-def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld):
+@pytest.mark.parametrize("m,n,P,Ld,grid", [(64, 32, 2, 2, None), (96, 32, 3, 2, None), (128, 64, 2, 3, None),
+                                           (64, 64, 4, 2, (2, 2)), (64, 128, 2, 2, (1, 2)),
+                                           (128, 96, 6, 2, (2, 3))])
+def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld, grid):
+    """Row slabs and 2-D blocks (x-then-y halo exchange, corners via the diagonal neighbours) over gloo,
+    world sizes 2..6, against the oracle's single-grid V-cycle on the global grid."""
     import dd_oracle
-    mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path)), nprocs=P, join=True)
-    got = np.concatenate([np.load(os.path.join(tmp_path, f"rank{r}.npy")) for r in range(P)], axis=1)
+    mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path), grid), nprocs=P, join=True)
+    got = np.full((2, m + 1, n + 1), np.nan)
+    for r in range(P):
+        s, e, sc, ec = map(int, open(os.path.join(tmp_path, f"rank{r}.idx")).read().split())
+        got[:, s:e, sc:ec] = np.load(os.path.join(tmp_path, f"rank{r}.npy"))
     f, u = dd_oracle.problem(m, n, 2)
     L = global_levels(m, n)
     mg = orc.OracleMultigrid(n, "poisson", np.float64, levels=L, rows=m)
@@ -126,5 +133,28 @@ def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld):
     v = u
     for _ in range(2):
         v = mg.step(v, f)
-    err = np.abs(got - v[:, 1:-1]).max() / np.abs(v).max()
+    inner = got[:, 1:-1, 1:-1]
+    assert not np.isnan(inner).any(), "owned blocks do not tile the interior"
+    err = np.abs(inner - v[:, 1:-1, 1:-1]).max() / np.abs(v).max()
     assert err < 1e-13, err
+
+
+def test_partition_2d():
+    """2-D blocks: both axes tile the interior exactly once, the column axis pairs fine and coarse
+    columns like the rows, default grids split rows at least as finely as columns."""
+    from feanet_amd.dd import Partition2D, default_grid
+    assert default_grid(8) == (4, 2) and default_grid(4) == (2, 2) and default_grid(2) == (2, 1)
+    part = Partition2D(8192, 8192, 4, 2, 4, 3)
+    for l in range(5):
+        W = (8192 >> l) + 1
+        cols = []
+        for r in range(8):
+            q = part.clevel(l, r)
+            if r // 2 == 0:
+                cols += list(range(q.s, q.e))
+            assert 0 <= q.gr0 and q.gr0 + q.Hloc <= W
+            if l < 4:  # intergrid levels need odd extents (the agglomerated level Ld does not)
+                assert q.Hloc % 2 == 1
+                q1 = part.clevel(l + 1, r)
+                assert q.gr0 == 2 * q1.gr0 and q.Hloc == 2 * q1.Hloc - 1
+        assert cols == list(range(1, W - 1))

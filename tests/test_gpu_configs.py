@@ -2,7 +2,7 @@
 against the single-GPU path, at the configuration's own size.
   C2  1025^2 Poisson fp64, 6-level V-cycle                      -> oracle, every cycle, 1e-10
   C3  2049^2 two-material, learned R/P ratio (multigrid.py)     -> oracle first cycle + convergence
-  C4  8193^2 Poisson fp64 over 8 row slabs (domain decomposed)  -> bitwise the single-GPU V-cycle
+  C4  8193^2 Poisson fp64 over 8 ranks (slabs, 4 x 2 blocks)   -> bitwise the single-GPU V-cycle
   C5  256 x 1025^2 fp32 batch                                   -> bitwise per-sample independence
 """
 import os
@@ -78,7 +78,9 @@ def test_c3_2049_interface_learned_ratio():
     assert r[-1] / r0 < 0.05, r
 
 
-def test_c4_8193_dd_eight_slabs_bitwise():
+@pytest.mark.parametrize("grid", [(8, 1), (4, 2)])
+def test_c4_8193_dd_eight_ranks_bitwise(grid):
+    """C4: 8193^2 over 8 ranks (row slabs, and the 4 x 2 blocks bench.py runs on 8 GPUs), in-process."""
     from feanet_amd.dd import LocalGroup
     from feanet_amd.solver import MultigridSolver
     n = 8192
@@ -88,7 +90,7 @@ def test_c4_8193_dd_eight_slabs_bitwise():
     s = MultigridSolver(n, dtype=torch.float64)
     s.set_rhs(f=f)
     s.load()
-    grp = LocalGroup(n, n, 8)
+    grp = LocalGroup(n, n, 8, grid=grid)
     grp.set_rhs(f)
     grp.load()
     for k in range(2):

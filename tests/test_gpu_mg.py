@@ -124,7 +124,7 @@ def test_mg_sweep(T, problem, n, B, nt):
     ws = torch.zeros(_lib.norm_workspace_bytes(B, fr.H, fr.W) // 8 + 1, dtype=torch.float64, device="cuda")
     res = torch.zeros(B, dtype=torch.float64, device="cuda")
     _lib.call("mg_residual_norm", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), fr.pid(), kt.data_ptr(), nt, res.data_ptr(),
-              ws.data_ptr(), *fr.args(), 0, 0, None)
+              ws.data_ptr(), *fr.args(), 0, 0, 0, 0, None)
     np.testing.assert_allclose(res.cpu().numpy(), orc.interior_norm(f - orc.knet_apply(u, fr.pid_np, ktab)),
                                rtol=1e-5 if T == torch.float32 else 1e-12)
 
@@ -576,12 +576,14 @@ def test_mg_rect_kernels(T, m, n, B):
     res = torch.zeros(B, dtype=torch.float64, device="cuda")
     r = f - orc.knet_apply(u, fr.pid_np, ktab)
     for lo, hi in ((0, 0), (1, H - 1), (2, max(2, H // 2)), (H // 2, H - 1), (3, 3)):
-        _lib.call("mg_residual_norm", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), None, kt.data_ptr(), 1, res.data_ptr(),
-                  ws.data_ptr(), *fr.args(), lo, hi, None)
-        a, b = (1, H - 1) if (lo, hi) == (0, 0) else (lo, hi)
-        ref = np.sqrt((r[:, a:b, 1:-1].astype(np.float64) ** 2).sum(axis=(1, 2)))
-        np.testing.assert_allclose(res.cpu().numpy(), ref, rtol=1e-5 if T == torch.float32 else 1e-12,
-                                   err_msg=f"norm rows {lo}:{hi}")
+        for clo, chi in ((0, 0), (1, W - 1), (2, max(2, W // 2)), (W // 3, W - 1)):
+            _lib.call("mg_residual_norm", T, fr.L.a.data_ptr(), fr.L.f.data_ptr(), None, kt.data_ptr(), 1,
+                      res.data_ptr(), ws.data_ptr(), *fr.args(), lo, hi, clo, chi, None)
+            a, b = (1, H - 1) if (lo, hi) == (0, 0) else (lo, hi)
+            c, d = (1, W - 1) if (clo, chi) == (0, 0) else (clo, chi)
+            ref = np.sqrt((r[:, a:b, c:d].astype(np.float64) ** 2).sum(axis=(1, 2)))
+            np.testing.assert_allclose(res.cpu().numpy(), ref, rtol=1e-5 if T == torch.float32 else 1e-12,
+                                       err_msg=f"norm rows {lo}:{hi} cols {clo}:{chi}")
 
 
 @pytest.mark.parametrize("T", [torch.float64, torch.float32])
