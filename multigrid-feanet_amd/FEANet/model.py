@@ -63,18 +63,50 @@ class KNet(nn.Module):
             raise RuntimeError(f"KNet: input dtype {x.dtype} != weight dtype {w.dtype} (use .double())")
         return w[0]
 
+    def _check_padded(self, x, what):
+        if x.shape[-2] != self.nnode_edge + 2 or x.shape[-1] != self.nnode_edge + 2:
+            raise ValueError(f"KNet.{what}: input must be N x N or (N+2) x (N+2) (N = {self.nnode_edge})")
+
+    def _padded_pid(self, x):
+        """Pattern map of an (N+2)^2 input: the interior carries the mesh's patterns; on the padding ring
+        every mask is 1 (model.py:26-28: F.pad(global_pattern, (1,1,1,1), 'constant', 1))."""
+        pp = getattr(self, "_pid_pad", None)
+        if pp is None or pp.device != x.device:
+            pp = torch.nn.functional.pad(self._pid(x)[None, None].float(), (1, 1, 1, 1))[0, 0].to(torch.uint8)
+            self._pid_pad = pp
+        return pp
+
+    @staticmethod
+    def _ring(x):
+        """(interior part, padding-ring part) of a padded field: x = a + b."""
+        inner = torch.zeros_like(x)
+        inner[..., 1:-1, 1:-1] = x[..., 1:-1, 1:-1]
+        return inner, x - inner
+
     def forward(self, u):
         H = u.shape[-2]
         if H != self.nnode_edge:
-            if self.n_channel != 1 or H != self.nnode_edge + 2:
-                raise NotImplementedError("KNet: padded inputs are supported for single-pattern meshes only")
-            return ops.knet_apply(u, self._tables(u), None)
+            # padded input (JacobiBlockPBC's circular extension, model.py:26-28): on the padding ring every
+            # mask is 1, so ring nodes act through the SUM of the pattern stencils; interior nodes through
+            # their own pattern's.  K u = K_pid(u inside) + K_sum(u on the ring) — one stencil each.
+            self._check_padded(u, "forward")
+            tab = self._tables(u)
+            if self.n_channel == 1:
+                return ops.knet_apply(u, tab, None)
+            inner, ring = self._ring(u)
+            return (ops.knet_apply(inner, tab, self._padded_pid(u))
+                    + ops.knet_apply(ring, tab.sum(0, keepdim=True), None))
         return ops.knet_apply(u, self._tables(u), self._pid(u) if self.n_channel > 1 else None)
 
     def split_x(self, x):
-        """x_split[:, p] = mask_p * x (model.py:37-47)."""
+        """x_split[:, p] = mask_p * x (model.py:37-47); on the ring of a padded (N+2)^2 input every
+        channel carries x (masks padded with 1, model.py:42-46)."""
         if x.shape[-2] != self.nnode_edge:
-            raise NotImplementedError("KNet.split_x: padded inputs are not supported")
+            self._check_padded(x, "split_x")
+            if self.n_channel == 1:
+                return ops.split_x(x, None, 1)
+            inner, ring = self._ring(x)
+            return ops.split_x(inner, self._padded_pid(x), self.n_channel) + ring
         return ops.split_x(x, self._pid(x) if self.n_channel > 1 else None, self.n_channel)
 
 

@@ -55,6 +55,24 @@ def _stencil_grad(g, u, ktab, pid, scale=1.0):
     return gw.reshape(ktab.shape).to(ktab.dtype)
 
 
+# Backward bodies shared by the torch.library registrations of torch_ops.py (the product path) and
+# the autograd.Function classes below (kept as a reference path for the tests).  Each reads what its
+# forward saved (ctx.saved_tensors, scalars on ctx) and returns one gradient per op input.
+
+def knet_backward(ctx, g):  # saved (u, ktab, pid)
+    u, ktab, pid = ctx.saved_tensors
+    gu = _knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
+    gk = _stencil_grad(g, u, ktab, pid) if ctx.needs_input_grad[1] else None
+    return gu, gk, None
+
+
+def residual_backward(ctx, g):  # saved (u, ktab, pid)
+    u, ktab, pid = ctx.saved_tensors
+    gu = -_knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
+    gk = _stencil_grad(g, u, ktab, pid, -1.0) if ctx.needs_input_grad[2] else None
+    return gu, (g if ctx.needs_input_grad[1] else None), gk, None
+
+
 class KNetApply(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u, ktab, pid):
@@ -63,10 +81,7 @@ class KNetApply(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        u, ktab, pid = ctx.saved_tensors
-        gu = _knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
-        gk = _stencil_grad(g, u, ktab, pid) if ctx.needs_input_grad[1] else None
-        return gu, gk, None
+        return knet_backward(ctx, g)
 
 
 class Residual(torch.autograd.Function):
@@ -77,10 +92,7 @@ class Residual(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        u, ktab, pid = ctx.saved_tensors
-        gu = -_knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
-        gk = _stencil_grad(g, u, ktab, pid, -1.0) if ctx.needs_input_grad[2] else None
-        return gu, (g if ctx.needs_input_grad[1] else None), gk, None
+        return residual_backward(ctx, g)
 
 
 class JacobiSweep(torch.autograd.Function):
@@ -94,29 +106,33 @@ class JacobiSweep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        _frozen(ctx, "omega-over-d / geometry / boundary values", 3, 5, 6)
-        u, ktab, omd, pid, geo, bc = ctx.saved_tensors
-        g = g.contiguous()
-        B, H, W = ops._bhw(g)
-        tab = ops._table(ktab, g.dtype, g.device)
-        om = torch.as_tensor(omd).to(device=g.device, dtype=g.dtype).reshape(-1).contiguous()
-        geo_t, gs = ops._bcast_stride(geo, B, H, W, "geometry_idx", g.dtype, g.device)
-        gu = torch.empty_like(g)
-        need_gf = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        gf = torch.empty_like(g) if need_gf else None
-        _lib.call("jacobi_sweep_adj", g.dtype, g.data_ptr(), gu.data_ptr(), ops._ptr(gf), ops._ptr(pid),
-                  tab.data_ptr(), om.data_ptr(), tab.shape[0], ops._ptr(geo_t), gs, B, H, W, ops._stream(g))
-        gk = None
-        if ctx.needs_input_grad[2]:  # d/dW of -sum(gf . K u0)
-            if geo is None:
-                u0 = u * _interior_mask(H, W, u)
-            else:
-                u0 = u * geo
-            if bc is not None:
-                u0 = u0 + bc
-            gk = _stencil_grad(gf, u0.to(g.dtype).expand(g.shape), ktab, pid, -1.0)
-        return (gu if ctx.needs_input_grad[0] else None), (gf if ctx.needs_input_grad[1] else None), gk, \
-            None, None, None, None
+        return jacobi_backward(ctx, g)
+
+
+def jacobi_backward(ctx, g):  # saved (u, ktab, omd, pid, geo, bc)
+    _frozen(ctx, "omega-over-d / geometry / boundary values", 3, 5, 6)
+    u, ktab, omd, pid, geo, bc = ctx.saved_tensors
+    g = g.contiguous()
+    B, H, W = ops._bhw(g)
+    tab = ops._table(ktab, g.dtype, g.device)
+    om = torch.as_tensor(omd).to(device=g.device, dtype=g.dtype).reshape(-1).contiguous()
+    geo_t, gs = ops._bcast_stride(geo, B, H, W, "geometry_idx", g.dtype, g.device)
+    gu = torch.empty_like(g)
+    need_gf = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+    gf = torch.empty_like(g) if need_gf else None
+    _lib.call("jacobi_sweep_adj", g.dtype, g.data_ptr(), gu.data_ptr(), ops._ptr(gf), ops._ptr(pid),
+              tab.data_ptr(), om.data_ptr(), tab.shape[0], ops._ptr(geo_t), gs, B, H, W, ops._stream(g))
+    gk = None
+    if ctx.needs_input_grad[2]:  # d/dW of -sum(gf . K u0)
+        if geo is None:
+            u0 = u * _interior_mask(H, W, u)
+        else:
+            u0 = u * geo
+        if bc is not None:
+            u0 = u0 + bc
+        gk = _stencil_grad(gf, u0.to(g.dtype).expand(g.shape), ktab, pid, -1.0)
+    return (gu if ctx.needs_input_grad[0] else None), (gf if ctx.needs_input_grad[1] else None), gk, \
+        None, None, None, None
 
 
 def _interior_mask(H, W, like):
@@ -134,14 +150,18 @@ class SplitX(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        (pid,) = ctx.saved_tensors
-        B, C, H, W = g.shape
-        if pid is None:
-            gx = g[:, :1]
-        else:  # the masks partition the nodes: d x_i = g[pid(i)]_i
-            idx = pid.to(torch.int64).reshape(1, 1, H, W).expand(B, 1, H, W)
-            gx = torch.gather(g, 1, idx)
-        return gx.reshape(ctx.xshape), None, None
+        return split_backward(ctx, g)
+
+
+def split_backward(ctx, g):  # saved (pid,), ctx.xshape
+    (pid,) = ctx.saved_tensors
+    B, C, H, W = g.shape
+    if pid is None:
+        gx = g[:, :1]
+    else:  # the masks partition the nodes: d x_i = g[pid(i)]_i
+        idx = pid.to(torch.int64).reshape(1, 1, H, W).expand(B, 1, H, W)
+        gx = torch.gather(g, 1, idx)
+    return gx.reshape(ctx.xshape).contiguous(), None, None
 
 
 def _weight_grad(cf, c_split, ff, f_split, C, interior, scale, Hc, Wc):
@@ -162,24 +182,29 @@ class Restrict(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        x, rtab, pid = ctx.saved_tensors
-        x = x.contiguous()
-        g = _like(g, x)
-        B, C, H, W = x.shape
-        Hc, Wc = (H + 1) // 2, (W + 1) // 2
-        tab = ops._table(rtab, x.dtype, x.device)
-        gx = gr = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.empty_like(x)
-            pp = pid if C == 1 else None
-            _lib.call("restrict_adj", x.dtype, g.data_ptr(), C, gx.data_ptr(), ops._ptr(pp), tab.data_ptr(),
-                      tab.shape[0], ctx.w0, B, H, W, ops._stream(x))
-        if ctx.needs_input_grad[1]:
-            if C == 1 and tab.shape[0] > 1:
-                raise NotImplementedError("feanet_amd: no kernel gradient in per-pattern (pid) restriction mode")
-            gr = _weight_grad(g, False, x, True, C, True, ctx.w0, Hc, Wc)
-            gr = gr.reshape(rtab.shape).to(rtab.dtype)
-        return gx, gr, None, None
+        return restrict_backward(ctx, g)
+
+
+def restrict_backward(ctx, g):  # saved (x, rtab, pid), ctx.w0
+    x, rtab, pid = ctx.saved_tensors
+    x = x.contiguous()
+    g = _like(g, x)
+    B, C, H, W = x.shape
+    Hc, Wc = (H + 1) // 2, (W + 1) // 2
+    tab = ops._table(rtab, x.dtype, x.device)
+    gx = gr = None
+    if ctx.needs_input_grad[0]:
+        gx = torch.empty_like(x)
+        pp = pid if C == 1 else None
+        _lib.call("restrict_adj", x.dtype, g.data_ptr(), C, gx.data_ptr(), ops._ptr(pp), tab.data_ptr(),
+                  tab.shape[0], ctx.w0, B, H, W, ops._stream(x))
+    if ctx.needs_input_grad[1]:
+        if C == 1 and tab.shape[0] > 1:
+            raise NotImplementedError("feanet_amd: no kernel gradient in per-pattern (pid) restriction mode")
+        gr = _weight_grad(g, False, x, True, C, True, ctx.w0, Hc, Wc)
+        gr = gr.reshape(rtab.shape).to(rtab.dtype)
+    return gx, gr, None, None
+
 
 
 class Prolong(torch.autograd.Function):
@@ -191,21 +216,25 @@ class Prolong(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        e, ptab, pidc = ctx.saved_tensors
-        e = e.contiguous()
-        g = _like(g, e)
-        B, C, Hc, Wc = e.shape
-        tab = ops._table(ptab, e.dtype, e.device)
-        ge = gp = None
-        if ctx.needs_input_grad[0]:
-            ge = torch.empty_like(e)
-            pp = pidc if C == 1 else None
-            _lib.call("prolong_adj", e.dtype, g.data_ptr(), C, ge.data_ptr(), ops._ptr(pp), tab.data_ptr(),
-                      tab.shape[0], ctx.w1, B, Hc, Wc, ops._stream(e))
-        if ctx.needs_input_grad[1]:
-            if C == 1 and tab.shape[0] > 1:
-                raise NotImplementedError("feanet_amd: no kernel gradient in per-pattern (pid) prolongation mode")
-            gp = _weight_grad(e, True, g, False, C, False, ctx.w1, Hc, Wc)
-            gp = gp.reshape(ptab.shape).to(ptab.dtype)
-        gadd = g if ctx.needs_input_grad[4] else None
-        return ge, gp, None, None, gadd
+        return prolong_backward(ctx, g)
+
+
+def prolong_backward(ctx, g):  # saved (e, ptab, pidc), ctx.w1
+    e, ptab, pidc = ctx.saved_tensors
+    e = e.contiguous()
+    g = _like(g, e)
+    B, C, Hc, Wc = e.shape
+    tab = ops._table(ptab, e.dtype, e.device)
+    ge = gp = None
+    if ctx.needs_input_grad[0]:
+        ge = torch.empty_like(e)
+        pp = pidc if C == 1 else None
+        _lib.call("prolong_adj", e.dtype, g.data_ptr(), C, ge.data_ptr(), ops._ptr(pp), tab.data_ptr(),
+                  tab.shape[0], ctx.w1, B, Hc, Wc, ops._stream(e))
+    if ctx.needs_input_grad[1]:
+        if C == 1 and tab.shape[0] > 1:
+            raise NotImplementedError("feanet_amd: no kernel gradient in per-pattern (pid) prolongation mode")
+        gp = _weight_grad(e, True, g, False, C, False, ctx.w1, Hc, Wc)
+        gp = gp.reshape(ptab.shape).to(ptab.dtype)
+    gadd = g if ctx.needs_input_grad[4] else None
+    return ge, gp, None, None, gadd

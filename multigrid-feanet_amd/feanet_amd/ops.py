@@ -192,20 +192,18 @@ def residual_norm(u, f=None, ktab=None, pid=None):
 
 
 # ---------------------------------------------------------------------------- public entry points
-# Each op runs its HIP kernel directly, or through the torch.autograd.Function of autograd.py
-# (HIP forward + HIP adjoint) when autograd has to record it: as with the reference's conv2d
-# modules, any input (field or weight table) that requires grad starts a graph.
+# The differentiable operators go through their PyTorch custom ops (torch.ops.feanet.*, torch_ops.py):
+# the registered implementation is the HIP kernel call above, the registered autograd its HIP adjoint.
 
-def _grad(*ts):
-    return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+def _T():
+    from . import torch_ops  # noqa: F401  (registers torch.ops.feanet.*)
+    return torch.ops.feanet
 
 
 def knet_apply(u, ktab, pid=None):
     """y = K u with per-node-pattern stencils (KNet.forward, FEANet/model.py:22-30)."""
-    if _grad(u, ktab):
-        from . import autograd
-        return autograd.KNetApply.apply(u, ktab, pid)
-    return _knet_apply(u, ktab, pid)
+    require_hip(u, "u")
+    return _T().knet_apply(u, ktab, pid)
 
 
 def conv3x3(x, w):
@@ -215,19 +213,16 @@ def conv3x3(x, w):
 
 def split_x(x, pid, C):
     """x_split[:, p] = mask_p * x (KNet.split_x, FEANet/model.py:37-47); x is [B, 1, H, W]."""
-    if _grad(x):
-        from . import autograd
-        return autograd.SplitX.apply(x, pid, C)
-    return _split_x(x, pid, C)
+    require_hip(x, "x")
+    return _T().split_x(x, pid, int(C))
 
 
 def jacobi_sweep(u, f, ktab, omd, pid=None, geo=None, bc=None):
     """One weighted-Jacobi sweep with Dirichlet reset (JacobiBlock.jacobi_convolution,
     FEANet/jacobi.py:39-47).  geo/bc None = square domain / zero boundary values."""
-    if _grad(u, f, ktab, omd, geo, bc):
-        from . import autograd
-        return autograd.JacobiSweep.apply(u, f, ktab, omd, pid, geo, bc)
-    return _jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
+    require_hip(u, "u")
+    omd = torch.as_tensor(omd, device=u.device)
+    return _T().jacobi_sweep(u, f, ktab, omd, pid, geo, bc)
 
 
 def pbc_pad(u, lo, hi):
@@ -265,27 +260,21 @@ def jacobi_sweep_pbc(u, f, ktab, omd):
 
 def residual(u, f, ktab, pid=None):
     """r = f - K u."""
-    if _grad(u, f, ktab):
-        from . import autograd
-        return autograd.Residual.apply(u, f, ktab, pid)
-    return _residual(u, f, ktab, pid)
+    require_hip(u, "u")
+    return _T().residual(u, f, ktab, pid)
 
 
 def restrict(x, rtab, w0=1.0, pid=None):
     """Restriction (RestrictionNet + MultiGrid.Restrict, FEANet/multigrid.py:50-60,115-122):
     x [B, C, H, W]; C > 1 means x is already split (one kernel per channel); C == 1 uses
     the kernel of each fine node's pattern (pid) or rtab[0].  Differentiable in x and rtab."""
-    if _grad(x, rtab):
-        from . import autograd
-        return autograd.Restrict.apply(x, rtab, w0, pid)
-    return _restrict(x, rtab, w0, pid)
+    require_hip(x, "x")
+    return _T().restrict(x, rtab, float(w0), pid)
 
 
 def prolong(e, ptab, w1=1.0, pidc=None, add=None):
     """Prolongation (ProlongationNet + MultiGrid.Interpolate, FEANet/multigrid.py:62-73,124-130):
     out = add + w1 * conv_transpose2d(e, P, stride 2, pad 1); e [B, C, Hc, Wc].
     Differentiable in e, ptab and add."""
-    if _grad(e, ptab, add):
-        from . import autograd
-        return autograd.Prolong.apply(e, ptab, w1, pidc, add)
-    return _prolong(e, ptab, w1, pidc, add)
+    require_hip(e, "e")
+    return _T().prolong(e, ptab, float(w1), pidc, add)

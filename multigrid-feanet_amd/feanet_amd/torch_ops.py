@@ -3,11 +3,13 @@
 BASELINE.json's north star asks for the kernels to be "surfaced to the Python host as PyTorch-ROCm
 custom ops".  Each op below is registered with torch.library for the HIP ('cuda') device only; its
 implementation is the ctypes call of feanet_amd.ops (one HIP kernel, the caller's current stream), a
-fake implementation gives output shapes for tracing / meta tensors, and knet_apply / residual carry
+fake implementation gives output shapes for tracing / meta tensors, and the differentiable ones carry
 their HIP adjoints (feanet_amd.autograd) through register_autograd.  CPU tensors find no kernel and
-raise — there is no CPU fallback.  The FEANet modules call feanet_amd.ops directly (same kernels).
+raise — there is no CPU fallback.  These ops ARE the product path of the generic operators: the
+FEANet drop-in modules and feanet_amd.ops' public functions call torch.ops.feanet.*.
 
   feanet::knet_apply(u, ktab, pid?)                   KNet.forward        FEANet/model.py:22-30
+  feanet::split_x(x, pid?, C)                         KNet.split_x        FEANet/model.py:37-47
   feanet::residual(u, f, ktab, pid?)                  f - K u             FEANet/multigrid.py:168
   feanet::jacobi_sweep(u, f, ktab, omd, pid?, geo?, bc?)  jacobi_convolution  FEANet/jacobi.py:39-47
   feanet::restrict(x, rtab, w0, pid?)                 MultiGrid.Restrict  FEANet/multigrid.py:115-122
@@ -42,14 +44,7 @@ def _knet_setup(ctx, inputs, output):
     ctx.save_for_backward(u, ktab, pid)
 
 
-def _knet_bwd(ctx, g):
-    u, ktab, pid = ctx.saved_tensors
-    gu = _ag._knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
-    gk = _ag._stencil_grad(g, u, ktab, pid) if ctx.needs_input_grad[1] else None
-    return gu, gk, None
-
-
-knet_apply.register_autograd(_knet_bwd, setup_context=_knet_setup)
+knet_apply.register_autograd(_ag.knet_backward, setup_context=_knet_setup)
 
 
 @torch.library.custom_op("feanet::residual", mutates_args=(), device_types=_DEV)
@@ -67,15 +62,7 @@ def _res_setup(ctx, inputs, output):
     ctx.save_for_backward(u, ktab, pid)
 
 
-def _res_bwd(ctx, g):
-    u, ktab, pid = ctx.saved_tensors
-    gu = -_ag._knet_adj(g, ktab, pid) if ctx.needs_input_grad[0] else None
-    gf = g if ctx.needs_input_grad[1] else None
-    gk = _ag._stencil_grad(g, u, ktab, pid, -1.0) if ctx.needs_input_grad[2] else None
-    return gu, gf, gk, None
-
-
-residual.register_autograd(_res_bwd, setup_context=_res_setup)
+residual.register_autograd(_ag.residual_backward, setup_context=_res_setup)
 
 
 @torch.library.custom_op("feanet::jacobi_sweep", mutates_args=(), device_types=_DEV)
@@ -89,6 +76,34 @@ def _(u, f, ktab, omd, pid=None, geo=None, bc=None):
     return torch.empty_like(u, memory_format=torch.contiguous_format)
 
 
+def _js_setup(ctx, inputs, output):
+    u, f, ktab, omd, pid, geo, bc = inputs
+    ctx.save_for_backward(u, ktab, omd, pid, geo, bc)
+
+
+jacobi_sweep.register_autograd(_ag.jacobi_backward, setup_context=_js_setup)
+
+
+@torch.library.custom_op("feanet::split_x", mutates_args=(), device_types=_DEV)
+def split_x(x: Tensor, pid: Optional[Tensor], C: int) -> Tensor:
+    return ops._split_x(x, pid, C)
+
+
+@split_x.register_fake
+def _(x, pid, C):
+    B, _, H, W = x.shape
+    return x.new_empty((B, C, H, W))
+
+
+def _split_setup(ctx, inputs, output):
+    x, pid, C = inputs
+    ctx.save_for_backward(pid)
+    ctx.xshape = x.shape
+
+
+split_x.register_autograd(_ag.split_backward, setup_context=_split_setup)
+
+
 @torch.library.custom_op("feanet::restrict", mutates_args=(), device_types=_DEV)
 def restrict(x: Tensor, rtab: Tensor, w0: float = 1.0, pid: Optional[Tensor] = None) -> Tensor:
     return ops._restrict(x, rtab, w0, pid)
@@ -98,6 +113,15 @@ def restrict(x: Tensor, rtab: Tensor, w0: float = 1.0, pid: Optional[Tensor] = N
 def _(x, rtab, w0=1.0, pid=None):
     B, _, H, W = x.shape
     return x.new_empty((B, 1, (H + 1) // 2, (W + 1) // 2))
+
+
+def _restrict_setup(ctx, inputs, output):
+    x, rtab, w0, pid = inputs
+    ctx.save_for_backward(x, rtab, pid)
+    ctx.w0 = float(w0)
+
+
+restrict.register_autograd(_ag.restrict_backward, setup_context=_restrict_setup)
 
 
 @torch.library.custom_op("feanet::prolong", mutates_args=(), device_types=_DEV)
@@ -110,6 +134,15 @@ def prolong(e: Tensor, ptab: Tensor, w1: float = 1.0, pidc: Optional[Tensor] = N
 def _(e, ptab, w1=1.0, pidc=None, add=None):
     B, _, Hc, Wc = e.shape
     return e.new_empty((B, 1, 2 * Hc - 1, 2 * Wc - 1))
+
+
+def _prolong_setup(ctx, inputs, output):
+    e, ptab, w1, pidc, add = inputs
+    ctx.save_for_backward(e, ptab, pidc)
+    ctx.w1 = float(w1)
+
+
+prolong.register_autograd(_ag.prolong_backward, setup_context=_prolong_setup)
 
 
 @torch.library.custom_op("feanet::residual_norm", mutates_args=(), device_types=_DEV)

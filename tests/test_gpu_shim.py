@@ -84,3 +84,30 @@ def test_multigrid_py_iterate(gold, on_gpu, tag, ncyc, path):
     assert len(hist) - 1 == ncyc
     np.testing.assert_allclose(hist[:8], g[f"{tag}_hist"][:8], rtol=3e-3, atol=1e-5 * hist[0])
     np.testing.assert_allclose(u.cpu().numpy(), g[f"{tag}_u"], atol=2e-4 * np.abs(g[f"{tag}_u"]).max())
+
+
+@pytest.mark.parametrize("shape", [0, 1])
+@pytest.mark.parametrize("T", [torch.float64, torch.float32])
+def test_knet_padded_multi_pattern(shape, T):
+    """KNet.forward / split_x on an (N+2)^2 input of a 16-pattern mesh: the reference pads every mask
+    with 1 (FEANet/model.py:26-28, 42-46).  Against that formulation in CPU PyTorch (conv2d identity
+    split, padded one-hot masks, conv2d stencils)."""
+    import torch.nn.functional as Fn
+    from FEANet.mesh import MeshCenterInterface
+    from FEANet.model import KNet
+    N = 17
+    mesh = MeshCenterInterface(2, [1, 20], N, shape)
+    kn = KNet(mesh).to(device="cuda", dtype=T)
+    u = torch.randn(2, 1, N + 2, N + 2, dtype=T, generator=torch.Generator().manual_seed(shape))
+    C = kn.n_channel
+    w1 = kn.net1.weight.detach().cpu()
+    w2 = kn.net2.weight.detach().cpu()
+    gp = Fn.pad(kn.global_pattern.cpu().to(T), (1, 1, 1, 1), "constant", 1)
+    split_ref = Fn.conv2d(u, w1, padding=1) * gp
+    y_ref = Fn.conv2d(split_ref, w2, padding=1)
+    tol = 1e-12 if T == torch.float64 else 2e-5
+    y = kn(u.cuda())
+    assert (y.cpu() - y_ref).abs().max() / y_ref.abs().max() < tol
+    sx = kn.split_x(u.cuda())
+    assert sx.shape == (2, C, N + 2, N + 2)
+    assert torch.equal(sx.cpu(), split_ref)

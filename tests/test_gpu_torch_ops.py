@@ -41,8 +41,44 @@ def test_custom_ops_equal_kernel_calls(T):
 def test_opcheck():
     import feanet_amd.torch_ops  # noqa: F401
     u, f, k = _data(torch.float64, N=17)
-    torch.library.opcheck(torch.ops.feanet.knet_apply.default, (u, k))
-    torch.library.opcheck(torch.ops.feanet.restrict.default, (u, k, 1.0))
+    F = torch.ops.feanet
+    omd = torch.tensor([0.25], dtype=torch.float64, device="cuda")
+    torch.library.opcheck(F.knet_apply.default, (u, k))
+    torch.library.opcheck(F.residual.default, (u, f, k))
+    torch.library.opcheck(F.restrict.default, (u, k, 1.0))
+    torch.library.opcheck(F.jacobi_sweep.default, (u, f, k, omd))
+    torch.library.opcheck(F.prolong.default, (F.restrict(u, k, 1.0), k, 1.0))
+    pid = (torch.arange(17 * 17, device="cuda") % 3).to(torch.uint8).reshape(17, 17)
+    torch.library.opcheck(F.split_x.default, (u, pid, 3))
+
+
+def test_all_differentiable_ops_match_functions():
+    """Every op with registered autograd (the product path of feanet_amd.ops and the FEANet modules) gives
+    the gradients of the autograd.Function reference path, bitwise."""
+    import feanet_amd.torch_ops  # noqa: F401
+    from feanet_amd import autograd as ag
+    u, f, k = _data(torch.float64, N=17, seed=4)
+    F = torch.ops.feanet
+    omd = torch.tensor([0.25], dtype=torch.float64, device="cuda")
+    pid = (torch.arange(17 * 17, device="cuda") % 3).to(torch.uint8).reshape(17, 17)
+    for which in ("jacobi", "split", "restrict", "prolong"):
+        grads = []
+        for path in ("custom", "function"):
+            uu, kk, ff = u.clone().requires_grad_(), k.clone().requires_grad_(), f.clone().requires_grad_()
+            if which == "jacobi":
+                y = F.jacobi_sweep(uu, ff, kk, omd) if path == "custom" else \
+                    ag.JacobiSweep.apply(uu, ff, kk, omd, None, None, None)
+            elif which == "split":
+                y = F.split_x(uu, pid, 3) if path == "custom" else ag.SplitX.apply(uu, pid, 3)
+            elif which == "restrict":
+                y = F.restrict(uu, kk, 0.5) if path == "custom" else ag.Restrict.apply(uu, kk, 0.5, None)
+            else:
+                e = uu[..., :9, :9]
+                y = F.prolong(e, kk, 1.5) if path == "custom" else ag.Prolong.apply(e, kk, 1.5, None, None)
+            y.backward(torch.ones_like(y))
+            grads.append([t.grad for t in (uu, kk, ff)])
+        for a, b in zip(*grads):
+            assert (a is None and b is None) or torch.equal(a, b), which
 
 
 def test_registered_autograd_matches_function():
