@@ -29,6 +29,21 @@ from . import ops
 _DEV = "cuda"
 
 
+def _full(bwd, n):
+    """A backward over all n schema inputs: the dispatcher drops trailing arguments equal to their
+    defaults (None pattern maps, geometry, ...) from what autograd tracks, so needs_input_grad is
+    padded for the shared backward bodies and the result trimmed back."""
+    def backward(ctx, g):
+        nig = tuple(ctx.needs_input_grad)
+        ctx.needs_input_grad = nig + (False,) * (n - len(nig))
+        try:
+            out = bwd(ctx, g)
+        finally:
+            ctx.needs_input_grad = nig
+        return tuple(out)[:len(nig)]
+    return backward
+
+
 @torch.library.custom_op("feanet::knet_apply", mutates_args=(), device_types=_DEV)
 def knet_apply(u: Tensor, ktab: Tensor, pid: Optional[Tensor] = None) -> Tensor:
     return ops._knet_apply(u, ktab, pid)
@@ -44,7 +59,7 @@ def _knet_setup(ctx, inputs, output):
     ctx.save_for_backward(u, ktab, pid)
 
 
-knet_apply.register_autograd(_ag.knet_backward, setup_context=_knet_setup)
+knet_apply.register_autograd(_full(_ag.knet_backward, 3), setup_context=_knet_setup)
 
 
 @torch.library.custom_op("feanet::residual", mutates_args=(), device_types=_DEV)
@@ -62,7 +77,7 @@ def _res_setup(ctx, inputs, output):
     ctx.save_for_backward(u, ktab, pid)
 
 
-residual.register_autograd(_ag.residual_backward, setup_context=_res_setup)
+residual.register_autograd(_full(_ag.residual_backward, 4), setup_context=_res_setup)
 
 
 @torch.library.custom_op("feanet::jacobi_sweep", mutates_args=(), device_types=_DEV)
@@ -81,7 +96,7 @@ def _js_setup(ctx, inputs, output):
     ctx.save_for_backward(u, ktab, omd, pid, geo, bc)
 
 
-jacobi_sweep.register_autograd(_ag.jacobi_backward, setup_context=_js_setup)
+jacobi_sweep.register_autograd(_full(_ag.jacobi_backward, 7), setup_context=_js_setup)
 
 
 @torch.library.custom_op("feanet::split_x", mutates_args=(), device_types=_DEV)
@@ -101,7 +116,7 @@ def _split_setup(ctx, inputs, output):
     ctx.xshape = x.shape
 
 
-split_x.register_autograd(_ag.split_backward, setup_context=_split_setup)
+split_x.register_autograd(_full(_ag.split_backward, 3), setup_context=_split_setup)
 
 
 @torch.library.custom_op("feanet::restrict", mutates_args=(), device_types=_DEV)
@@ -121,7 +136,7 @@ def _restrict_setup(ctx, inputs, output):
     ctx.w0 = float(w0)
 
 
-restrict.register_autograd(_ag.restrict_backward, setup_context=_restrict_setup)
+restrict.register_autograd(_full(_ag.restrict_backward, 4), setup_context=_restrict_setup)
 
 
 @torch.library.custom_op("feanet::prolong", mutates_args=(), device_types=_DEV)
@@ -142,7 +157,7 @@ def _prolong_setup(ctx, inputs, output):
     ctx.w1 = float(w1)
 
 
-prolong.register_autograd(_ag.prolong_backward, setup_context=_prolong_setup)
+prolong.register_autograd(_full(_ag.prolong_backward, 5), setup_context=_prolong_setup)
 
 
 @torch.library.custom_op("feanet::residual_norm", mutates_args=(), device_types=_DEV)
