@@ -266,6 +266,10 @@ def main():
     ap.add_argument("--weak", action="store_true",
                     help="dd: weak scaling instead, --n x --n intervals per GPU (4097^2, 8193x4097, 8193^2, 16385x8193)")
     ap.add_argument("--grid", default=None, help="dd: rank grid PRxPC (default: 2->2x1, 4->2x2, 8->4x2)")
+    ap.add_argument("--rhs", default=None, choices=["randn", "families"],
+                    help="right-hand side: seeded Gaussian assembled rhs, or nodal sources from the six "
+                         "families of the reference's Data/RHS/generate_rhs.py with FNet applied (default: "
+                         "families for batches, the BASELINE C5 inputs; randn otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     args = ap.parse_args()
@@ -276,6 +280,7 @@ def main():
     from feanet_amd.solver import MultigridSolver
     T = torch.float64 if args.dtype == "f64" else torch.float32
     n, B = args.n, args.batch
+    rhs = args.rhs or ("families" if B > 1 else "randn")
     g = torch.Generator(device="cuda")
     if mode == "dd":
         if args.problem != "poisson":
@@ -305,7 +310,11 @@ def main():
         N = n + 1
         s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
         g.manual_seed(1234 + rank)
-        s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
+        if rhs == "families":
+            from tools import rhs_families
+            s.set_rhs(F=rhs_families.batch(B, N, T, "cuda", seed=rank))
+        else:
+            s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
         dof = B * N * N * ws
         lvl = s
         workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics), "
@@ -381,7 +390,9 @@ def main():
         "scaling": "strong" if (mode == "dd" and not args.weak) else "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (seeded Gaussian rhs, zero initial guess)",
+        "data": ("synthetic (seeded Gaussian rhs, zero initial guess)" if rhs == "randn" else
+                 "synthetic (nodal sources from the six Data/RHS/generate_rhs.py families, seeded, FNet applied; "
+                 "zero initial guess)"),
         "config": {"workload": workload, "mode": mode, "batch": B, "levels": s.L, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "kernel": rkern,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -101,13 +101,17 @@ def test_c4_8193_dd_eight_ranks_bitwise(grid):
 
 
 def test_c5_batch256_1025_fp32():
+    """C5: 256 nodal sources from the six families of the reference's RHS generator
+    (Data/RHS/generate_rhs.py:6-56, tools/rhs_families.py), FNet applied on the device."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, ".."))
+    from tools import rhs_families
     from feanet_amd.solver import MultigridSolver
     n, B = 1024, 256
-    g = torch.Generator(device="cuda")
-    g.manual_seed(5)
-    f = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=torch.float32, generator=g)
+    F = rhs_families.batch(B, n + 1, torch.float32, "cuda", seed=5)
     s = MultigridSolver(n, dtype=torch.float32, batch=B)
-    s.set_rhs(f=f)
+    s.set_rhs(F=F)
+    f = s.levels[0].view(s.levels[0].f).unsqueeze(1).clone()
     s.load()
     r0 = s.residual_norm()
     s.vcycle(3)
