@@ -327,11 +327,10 @@ def main():
     conv = float((s.residual_norm().max() / r0.max()).item()) ** (1.0 / 8)
     s.load()
 
-    # warm-up: the timed call itself (vcycle(steps)), repeated so that it has started from both
-    # ping-pong buffers at least twice: every graph the timed call replays (its blocks of joined
-    # cycles, keyed by start buffer and size) has run once eagerly and been captured before the clock
-    # starts.  At least --warmup cycles in total.
-    calls = max(4, -(-args.warmup // args.steps))
+    # warm-up: the timed call itself (vcycle(steps)), repeated so that every graph the timed call
+    # replays (its blocks of joined cycles, keyed by start buffer and size; 5 calls cover every step
+    # count) has run once eagerly and been captured before the clock starts.  At least --warmup cycles.
+    calls = max(6, -(-args.warmup // args.steps))
     calls += calls % 2
     warm = 0
     for _ in range(calls):

@@ -218,6 +218,9 @@ class MultigridSolver:
                               device=dev)
         self.norm_out = torch.zeros(self.B, dtype=torch.float64, device=dev)
         self._state = "a"
+        # joinable solvers rest BETWEEN cycles in a pipelined ("mid-cycle") state after vcycle(k): see
+        # _vcycles_pipelined; None = the iterate is materialised in buffer self._state
+        self._mid = None
         self._hist = None  # solve(): fused residual-norm history + counters (_ensure_hist)
         self._cnt = None
         self._hist_gen = 0
@@ -263,6 +266,7 @@ class MultigridSolver:
             f = ops.conv3x3(F, torch.from_numpy(self.mass))
         f = self._check_field(f, "f")
         L0 = self.levels[0]
+        self._collapse()  # a pipelined next pre-smooth was made with the old right-hand side
         self._pack(f, L0.f, geo=None, bc=None, reset=False)
 
     def set_boundary(self, bc_value=None, geometry_idx=None):
@@ -299,6 +303,7 @@ class MultigridSolver:
             u0 = self._check_field(u0, "u0")
         self._pack(u0, L0.a, bc=bc)
         self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
+        self._mid = None
         if L0.c is not None and self._c_bc is not self._bc_version:
             self._pack(u0, L0.c, bc=bc)  # c only needs the Dirichlet values on its boundary nodes
             self._c_bc = self._bc_version
@@ -315,14 +320,14 @@ class MultigridSolver:
         """Current fine iterate as a contiguous [B, 1, H, W] tensor."""
         L0 = self.levels[0]
         out = torch.empty((self.B, 1, self.H, self.W), dtype=self.dtype, device=self.device)
-        _lib.call("mg_unpack", self.dtype, L0.buf(self._state).data_ptr(), out.data_ptr(), *L0.geom(),
+        _lib.call("mg_unpack", self.dtype, L0.buf(self._iterate()).data_ptr(), out.data_ptr(), *L0.geom(),
                   ops._stream(out))
         return out
 
     def residual_norm(self):
         """Per-sample ||(f - K u)[1:-1, 1:-1]||_2 of the current iterate (float64 device tensor [B])."""
         L0 = self.levels[0]
-        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(),
+        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._iterate()).data_ptr(), L0.f.data_ptr(),
                   None if L0.pid is None else L0.pid.data_ptr(), self.ktab.data_ptr(), self.ntab,
                   self.norm_out.data_ptr(), self.ws.data_ptr(), *L0.geom(), 0, 0, 0, 0,
                   torch.cuda.current_stream(self.device).cuda_stream)
@@ -530,32 +535,88 @@ class MultigridSolver:
                 r -= b
         return blocks
 
-    def _vcycles_joined(self, k):
-        """k >= 2 V-cycles with the cycle boundaries joined on the finest level (see join_cycles),
-        replayed as FEW HIP graphs whatever k is: the k - 1 joined cycles go in blocks of GRAPH_CYCLES
-        plus the binary decomposition of the remainder (graph_blocks); the first block also carries the
-        first cycle's head, the last block the last cycle's tail.  Each graph launch costs ~8 us of
-        dispatch gap on the GPU, so vcycle(20) pays it 3 times (16 + 2 + 1), vcycle(1000) 34 times.
-        A block's graph is keyed by (start buffer, size, head?, tail?): at most 2 x 2 x 2 x log2(G)+1
-        graphs, each captured on its second use."""
-        prog, end = self.joined_program(k)
+    def _ensure_c(self):
+        """The finest level's third buffer with the Dirichlet values on its boundary nodes (its interior is
+        always written before it is read)."""
+        L0 = self.levels[0]
+        if L0.c is None or self._c_bc is not self._bc_version:
+            L0.buf("c")
+            self._pack(None, L0.c, bc=getattr(self, "_bc", None))
+            self._c_bc = self._bc_version
+
+    def _collapse(self):
+        """Leave the pipelined state: the last cycle's end iterate recomputed (PS(0) from the join's
+        inputs) into the buffer of the now-discarded next pre-smooth, which becomes the resting state."""
+        m = self._mid
+        if m is None:
+            return
+        name, args = self._plan("a")[0][-1]
+        args = (self._ptr(0, m["last"]), args[1], args[2], self._ptr(0, m["pre"])) + args[4:]
+        self._launch([(name, args)])
+        self._state = m["pre"]
+        self._mid = None
+
+    def _iterate(self):
+        """Name of the finest-level buffer holding the current iterate.  In the pipelined state the
+        last cycle's end iterate v is not stored (the cycle join went on to the next pre-smooth): it is
+        recomputed once by the last post-smooth PS(0) from the join's inputs, still intact — the
+        pre-smoothed iterate `last` and the level-1 correction — into buffer c (bitwise the unjoined
+        cycle's result)."""
+        m = self._mid
+        if m is None:
+            return self._state
+        if not m["mat"]:
+            self._ensure_c()
+            name, args = self._plan("a")[0][-1]  # PS(0): (u, ec, f, out, ...)
+            args = (self._ptr(0, m["last"]), args[1], args[2], self._ptr(0, "c")) + args[4:]
+            self._launch([(name, args)])
+            m["mat"] = True
+        return "c"
+
+    def _vcycles_pipelined(self, k):
+        """k V-cycles as k x [levels >= 1 of a cycle + the cycle join] (fea_mg_cycle_join: post-smooth of
+        the cycle and pre-smooth + residual + restriction of the next, 28 instead of 52 B per fine node).
+        The solver rests between calls in the pipelined state the join leaves — the NEXT cycle's
+        pre-smoothed iterate in `pre`, its restricted residual in f_1 — so consecutive calls pay neither a
+        separate first pre-smooth nor a last post-smooth: every call, whatever k, runs exactly k cycles'
+        work at the steady-state rate.  From a loaded iterate the first call opens the pipeline with that
+        pre-smooth (fea_mg_sweep_restrict).  The end iterate is materialised only when asked for
+        (_iterate).  Replayed as few HIP graphs: blocks of GRAPH_CYCLES joins plus the binary
+        decomposition of the rest (graph_blocks), keyed by (pipeline opened?, buffer, size)."""
+        other = lambda b: "b" if b == "a" else "a"
+        plan, _ = self._plan("a")
+        mid = plan[1:-1]  # levels >= 1 (they never touch the finest level's iterate buffers)
+        ec_ptr = plan[-1][1][1]  # level-1 correction the finest prolongation reads (same every cycle)
+        if self._mid is None:
+            s0 = self._state
+            head = [self._plan(s0)[0][0]]
+            pre = other(s0)
+        else:
+            head, pre = [], self._mid["pre"]
         G = max(1, self.GRAPH_CYCLES)
         G = 1 << (G.bit_length() - 1)
-        head, joins, tail = prog[0], prog[1:-1], prog[-1]
-        blocks = self.graph_blocks(len(joins), G)
-        i = 0
-        for bi, nb in enumerate(blocks):
-            first, last = bi == 0, bi == len(blocks) - 1
-            segs = ([head] if first else []) + joins[i:i + nb] + ([tail] if last else [])
-            key = ("block", joins[i][0][1], nb, first, last)
-            self._run_segment(key, [ln for _, seg in segs for ln in seg])
-            i += nb
-        self._state = end
+        for nb in self.graph_blocks(k, G):
+            key = ("pipe", bool(head), pre, nb)
+            g = self._graphs.get(key)
+            if g is not None:
+                g.replay()
+                if nb % 2:
+                    pre = other(pre)
+            else:
+                launches = list(head)
+                for _ in range(nb):
+                    launches += mid + [self._join_call(pre, ec_ptr)]
+                    pre = other(pre)
+                self._run_segment(key, launches)
+            head = []
+        self._mid = {"pre": pre, "last": other(pre), "mat": False}
 
     def vcycle(self, k=1):
         """Run k V-cycles on the resident iterate (asynchronous; no host sync)."""
-        if k >= 2 and self._joinable() and not getattr(self, "_hjac_first", False):
-            self._vcycles_joined(k)
+        if k < 1:
+            return
+        if self._joinable() and not getattr(self, "_hjac_first", False):
+            self._vcycles_pipelined(k)
             return
         for _ in range(k):
             plan, end = self._plan(self._state)
@@ -662,10 +723,7 @@ class MultigridSolver:
         so the prediction errs short: another block costs one host round trip, an overshoot a re-run)."""
         self._ensure_hist(max_cycles + 2)
         L0, L1 = self.levels[0], self.levels[1]
-        if L0.c is None or self._c_bc is not self._bc_version:
-            L0.buf("c")
-            self._pack(None, L0.c, bc=getattr(self, "_bc", None))  # boundary values (interior: written first)
-            self._c_bc = self._bc_version
+        self._ensure_c()
 
         def stop(h):
             return (not np.all(np.isfinite(h))) or h.max() <= eps
@@ -793,20 +851,18 @@ class MultigridSolver:
 
     # ------------------------------------------------------------------ accounting
     def bytes_per_vcycle(self, k=1):
-        """Algorithmic HBM bytes per V-cycle of vcycle(k) as executed (DESIGN.md §3 accounting); with
-        joined cycles (k >= 2) the k-1 boundaries run fea_mg_cycle_join instead of PS(0) + SR(0)."""
+        """Algorithmic HBM bytes per V-cycle as executed (DESIGN.md §3 accounting).  Joinable solvers run
+        every cycle as [levels >= 1 + one fea_mg_cycle_join] (pipelined, _vcycles_pipelined)."""
         esz = 4 if self.dtype == torch.float32 else 8
-        plan = self._plan(self._state)[0]
-        one = self._plan_bytes(plan)
-        if k < 2 or not self._joinable():
-            return one
+        plan = self._plan("a")[0]
+        if not self._joinable():
+            return self._plan_bytes(plan)
         L0, L1 = self.levels[0], self.levels[1]
         nodes = L0.B * (L0.H - 2) * (L0.W - 2)
         coarse = L1.B * (L1.H - 2) * (L1.W - 2)
         pb = 1 if self.problem == "interface" else 0
         join = nodes * (3 * esz + pb) + coarse * (2 * esz + pb)
-        edge = self._plan_bytes([plan[0], plan[-1]])  # SR(0) + PS(0) replaced by one join per boundary
-        return (k * one - (k - 1) * edge + (k - 1) * join) / k
+        return self._plan_bytes(plan[1:-1]) + join
 
     def _plan_bytes(self, plan):
         esz = 4 if self.dtype == torch.float32 else 8

@@ -814,3 +814,35 @@ def test_solve_full_size_rate():
                                  for w, t in [(e[0], e[1]) if len(e) == 2 else (e[0], e[1:]) for e in s._solve_log]])
     s._trace = False
     assert t_solve < 1.10 * t_cyc + t_io + 5e-5, (t_solve, t_cyc, t_io)  # + one host round trip of slack
+
+
+def test_pipelined_state_semantics():
+    """Joinable solvers rest between vcycle() calls in the pipelined state (next pre-smooth done, end
+    iterate materialised on demand): solution() / residual_norm() between calls, a new right-hand side
+    mid-pipeline and vcycle(1) chains all give the unjoined sequence's iterates bitwise."""
+    from feanet_amd.solver import MultigridSolver
+    n, B = 256, 2
+    rng = np.random.default_rng(21)
+    f1 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    f2 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    out = []
+    for join in (False, True):
+        s = MultigridSolver(n, dtype=torch.float64, batch=B, join_cycles=join)
+        s.set_rhs(f=f1)
+        s.load(u0)
+        rec = []
+        s.vcycle(1)
+        rec.append(s.residual_norm())
+        s.vcycle(1)
+        s.vcycle(3)
+        rec.append(s.solution())
+        s.set_rhs(f=f2)  # the pipelined pre-smooth used f1: must be redone with f2
+        s.vcycle(2)
+        rec.append(s.solution())
+        rec.append(s.residual_norm())
+        s.vcycle(1)
+        rec.append(s.solution())
+        out.append(rec)
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
