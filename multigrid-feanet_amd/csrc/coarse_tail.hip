@@ -72,227 +72,300 @@ __device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element off
 
 
 // ---------------------------------------------------------------------------------------------
-// Fused V(1,1) coarse sub-cycle: one workgroup barrier per level and direction.  Wave w of the 16
-// owns a contiguous block of rows of each level, lane c is column c (levels are <= 65 wide; column
-// 64 is a boundary column, read as 0), horizontal neighbours come from DPP row shifts, vertical ones
-// from a sliding window of rows in registers — so a level's 9-point stencil costs ~1 LDS read per
-// node instead of 9.  Per level:
-//   down:   v = omd f (stored: the pre-smoothed iterate), r = f - K v on the rows the wave's coarse
-//           rows need (v recomputed there, it is pointwise), f_c = w0 R r       -> barrier
-//   coarsest: v1 = omd f, v2 = v1 + omd (f - K v1)                               -> barrier
-//   up:     x = v + w1 P e (rows the wave's sweep reads), v' = x + omd (f - K x) -> barrier
-//           (level 0: v' goes straight to HBM)
-// Every node value is the same expression, in the same order, as the general path (bitwise).
+// Fused V(1,1) coarse sub-cycle, laid out for latency: ONE workgroup barrier per level and
+// direction, and inside a phase every LDS load of a wave is issued up front (clamped addresses,
+// results masked by selects instead of branches) so the row chains run back to back instead of
+// waiting on one load at a time.  Wave w of the 16 owns a contiguous block of rows of each level,
+// lane c is column c (levels are <= 65 wide; column 64 is a boundary column, read as 0),
+// horizontal neighbours come from DPP row shifts, each row shifted once.  Per level:
+//   down:     v = omd f on the rows the wave's coarse rows need (pointwise, never stored),
+//             r = f - K v, f_c = w0 R r  (level 0 reads f_t straight from HBM)       -> barrier
+//   coarsest: v1 = omd f, v2 = v1 + omd (f - K v1)                                   -> barrier
+//   up:       x = omd f + w1 P e on the rows the wave's sweep reads (the zero-guess pre-smoothed
+//             iterate recomputed, as the streaming kernels do), v' = x + omd (f - K x) -> barrier
+//             (level 0: v' goes straight to HBM)
+// Every node value is the same expression, in the same order, as the general path (bitwise):
+// acc chains start from 0 and add the taps in (row, column) order; x = fma(w1, P e, omd f).
 // ---------------------------------------------------------------------------------------------
+constexpr int kTailDownRows = 2;  // coarse rows per wave going down: Hc - 2 <= 31 over 16 waves
+constexpr int kTailUpRows = 4;    // fine rows per wave going up / at the coarsest level: H - 2 <= 63
+
 template <typename T, bool MULTI>
-__device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* va, T* vb, T* fs, const T* ktb, const T* rtb,
+struct TailFast {
+  const TailArgs<T>& a;
+  T* es;               // per-level corrections (up-sweep outputs), level regions like fs
+  T* fs;               // per-level right-hand sides
+  const T* ktb;        // LDS tables (MULTI)
+  const T* rtb;
+  const T* ptb;
+  const uint8_t* pl;   // LDS pattern maps (MULTI)
+  const T* fg;         // row 0 of this sample's f_t (framed, HBM)
+  T* vg;               // row 0 of this sample's v_t
+  int ld, wv, lane;
+  T kr[9], rr[9], pr[9], om0;
+
+  __device__ __forceinline__ T omega(int p) const {
+    if constexpr (MULTI) return ktb[p * kTS + 9];
+    return om0;
+  }
+  __device__ __forceinline__ T kw(int p, int d) const {
+    if constexpr (MULTI) return ktb[p * kTS + d];
+    return kr[d];
+  }
+  __device__ __forceinline__ T rw(int p, int d) const {
+    if constexpr (MULTI) return rtb[p * kTS + d];
+    return rr[d];
+  }
+  __device__ __forceinline__ T pw(int p, int d) const {
+    if constexpr (MULTI) return ptb[p * kTS + d];
+    return pr[d];
+  }
+  __device__ __forceinline__ bool inside(int H, int N, int y) const {
+    return y >= 1 && y <= H - 2 && lane >= 1 && lane <= N - 2;
+  }
+  // pattern id of node (y, lane) of a level (0 off the level), loaded unconditionally
+  __device__ __forceinline__ int pat(const uint8_t* pk, int H, int N, int y) const {
+    if constexpr (MULTI) {
+      const int p = pk[min(max(y, 0), H - 1) * N + min(lane, N - 1)];
+      return (y >= 0 && y < H && lane < N) ? p : 0;
+    }
+    return 0;
+  }
+  // (K x) on row j of a register window: rows j-1..j+1 with their DPP-shifted copies
+  template <int R>
+  __device__ __forceinline__ T Kx(int j, const T (&xl)[R], const T (&x)[R], const T (&xr)[R], const int (&ql)[R],
+                                  const int (&q)[R], const int (&qr)[R]) const {
+    T acc = 0;
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      acc += kw(ql[j - 1 + dr], dr * 3 + 0) * xl[j - 1 + dr];
+      acc += kw(q[j - 1 + dr], dr * 3 + 1) * x[j - 1 + dr];
+      acc += kw(qr[j - 1 + dr], dr * 3 + 2) * xr[j - 1 + dr];
+    }
+    return acc;
+  }
+  template <int R>
+  __device__ __forceinline__ void shift(const T (&x)[R], T (&xl)[R], T (&xr)[R]) const {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      xl[j] = shr1z(x[j]);
+      xr[j] = shl1z(x[j]);
+    }
+  }
+  template <int R>
+  __device__ __forceinline__ void shift(const int (&q)[R], int (&ql)[R], int (&qr)[R]) const {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if constexpr (MULTI) {
+        ql[j] = shr1z(q[j]);
+        qr[j] = shl1z(q[j]);
+      } else {
+        ql[j] = qr[j] = 0;
+      }
+    }
+  }
+
+  // level k (offset o) -> f_{k+1}; GLOBAL: f_k is f_t in HBM (level 0)
+  template <bool GLOBAL>
+  __device__ __forceinline__ void down(int k, int o) const {
+    constexpr int kWaves = kTailThreads / 64;
+    constexpr int R = 2 * kTailDownRows + 3;
+    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    const T* f = fs + o;
+    const uint8_t* pk = pl + o;
+    T* fc = fs + o + H * N;
+    const int per = (Hc - 2 + kWaves - 1) / kWaves;
+    const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
+    if (I0 >= I1) return;  // wave-uniform
+    const int yb = 2 * I0 - 2;  // rows yb .. yb + R - 1 (residual rows yb + 1 .. yb + R - 2)
+    T fr[R], v[R], vl[R], vr[R], r[R], rl[R], rrt[R];
+    int q[R], ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int y = min(yb + j, H - 1);
+      if constexpr (GLOBAL) fr[j] = fg[(long long)y * ld + lane];
+      else fr[j] = f[y * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = inside(H, N, yb + j) ? omega(q[j]) * fr[j] : T(0);
+    shift(v, vl, vr);
+    shift(q, ql, qr);
+    r[0] = r[R - 1] = T(0);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const T kv = keep(Kx(j, vl, v, vr, ql, q, qr));
+      r[j] = inside(H, N, yb + j) ? fr[j] - kv : T(0);
+    }
+    shift(r, rl, rrt);
+    const int J = lane >> 1;
+    const bool st = !(lane & 1) && J >= 1 && J <= Nc - 2;
+#pragma unroll
+    for (int i = 0; i < kTailDownRows; ++i) {
+      if (I0 + i >= I1) break;
+      T acc = 0;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int j = 2 * i + 1 + ky;
+        acc += rw(ql[j], ky * 3 + 0) * rl[j];
+        acc += rw(q[j], ky * 3 + 1) * r[j];
+        acc += rw(qr[j], ky * 3 + 2) * rrt[j];
+      }
+      acc = keep(acc);
+      if (st) fc[(I0 + i) * Nc + J] = a.w0 * acc;
+    }
+  }
+
+  // coarsest level k: v1 = omd f, v2 = v1 + omd (f - K v1)
+  __device__ __forceinline__ void coarsest(int k, int o) const {
+    constexpr int kWaves = kTailThreads / 64;
+    constexpr int R = kTailUpRows + 2;
+    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k);
+    const T* f = fs + o;
+    const uint8_t* pk = pl + o;
+    const int per = (H - 2 + kWaves - 1) / kWaves;
+    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+    if (y0 >= y1) return;
+    const int yb = y0 - 1;
+    T fr[R], v[R], vl[R], vr[R];
+    int q[R], ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      fr[j] = f[min(yb + j, H - 1) * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = inside(H, N, yb + j) ? omega(q[j]) * fr[j] : T(0);
+    shift(v, vl, vr);
+    shift(q, ql, qr);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const int y = yb + j;
+      if (y >= y1) break;
+      const T kv = Kx(j, vl, v, vr, ql, q, qr);
+      const T w = keep(omega(q[j]) * (fr[j] - kv) + v[j]);
+      if (inside(H, N, y)) {
+        if (k == 0) vg[(long long)y * ld + lane] = w;
+        else es[o + y * N + lane] = w;
+      }
+    }
+  }
+
+  // level k (offset o) from the correction of level k + 1 (offset oc): x = omd f + w1 P e, one sweep.
+  // PAR = parity of the wave's first window row, so every coarse-row index is a compile-time constant.
+  template <int PAR>
+  __device__ __forceinline__ void up_rows(int k, int o, int oc, int y0, int y1) const {
+    constexpr int R = kTailUpRows + 2;        // x rows y0-1 .. y0+R-2
+    constexpr int C = (PAR + R) / 2 + 1;      // coarse rows Ib .. Ib+C-1 that they touch
+    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    const T* f = fs + o;
+    const T* e = es + oc;
+    const uint8_t* pk = pl + o;
+    const uint8_t* pkc = pl + oc;
+    const int yb = y0 - 1, Ib = yb >> 1;  // yb = 2 Ib + PAR
+    const int Ja = (lane + 1) >> 1, Jb = (lane - 1) >> 1;  // even lane: Ja only (kx = 1); odd: Ja (kx = 0), Jb (kx = 2)
+    const bool odd = lane & 1;
+    T fr[R], ea[C], eb[C];
+    int q[R], pa[C], pb[C];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      fr[j] = f[min(yb + j, H - 1) * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int I = Ib + c, Ic = min(I, Hc - 1);
+      const bool iin = I >= 1 && I <= Hc - 2;
+      const int jA = min(Ja, Nc - 1), jB = max(Jb, 0);
+      const T va = e[Ic * Nc + jA], vb = e[Ic * Nc + jB];
+      ea[c] = (iin && Ja >= 1 && Ja <= Nc - 2) ? va : T(0);
+      eb[c] = (iin && Jb >= 1 && Jb <= Nc - 2) ? vb : T(0);
+      if constexpr (MULTI) {
+        pa[c] = pkc[Ic * Nc + jA];
+        pb[c] = pkc[Ic * Nc + jB];
+      } else {
+        pa[c] = pb[c] = 0;
+      }
+    }
+    T x[R], xl[R], xr[R];
+    int ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      T acc = 0;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        if ((PAR + j + 1 - ky) & 1) continue;  // coarse row (y + 1 - ky) / 2 exists only for even y + 1 - ky
+        const int c = (PAR + j + 1 - ky) >> 1;
+        const T cfa = odd ? pw(pa[c], ky * 3 + 0) : pw(pa[c], ky * 3 + 1);
+        const T t = acc + cfa * ea[c];
+        const T t2 = t + pw(pb[c], ky * 3 + 2) * eb[c];
+        acc = odd ? t2 : t;
+      }
+      const T v0 = omega(q[j]) * fr[j];
+      const T xv = keep(v0 + a.w1 * acc);
+      x[j] = inside(H, N, yb + j) ? xv : T(0);
+    }
+    shift(x, xl, xr);
+    shift(q, ql, qr);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const int y = yb + j;
+      if (y >= y1) break;
+      const T kx = Kx(j, xl, x, xr, ql, q, qr);
+      const T w = keep(omega(q[j]) * (fr[j] - kx) + x[j]);
+      if (inside(H, N, y)) {
+        if (k == 0) vg[(long long)y * ld + lane] = w;
+        else es[o + y * N + lane] = w;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void up(int k, int o, int oc) const {
+    constexpr int kWaves = kTailThreads / 64;
+    const int H = tail_n(a.Ht, k);
+    const int per = (H - 2 + kWaves - 1) / kWaves;
+    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+    if (y0 >= y1) return;
+    if ((y0 - 1) & 1) up_rows<1>(k, o, oc, y0, y1);
+    else up_rows<0>(k, o, oc, y0, y1);
+  }
+};
+
+template <typename T, bool MULTI>
+__device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, const T* ktb, const T* rtb,
                                           const T* ptb, const uint8_t* pl, int wv, int lane
 #ifdef FEA_TAIL_TRACE
                                           , int& nph
 #endif
 ) {
-  constexpr int kWaves = kTailThreads / 64;
   const int nlev = a.nlev, Ht = a.Ht, Wt = a.Wt;
-  // single-pattern tables in registers (uniform)
-  T kr[9], rr[9], pr[9], om0 = T(0);
-  if constexpr (!MULTI) {
+  const long long s0 = (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1) + a.ld_t;
+  TailFast<T, MULTI> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
+  if constexpr (!MULTI) {  // single-pattern tables in registers (uniform loads)
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-      kr[d] = ktb[d];
-      rr[d] = rtb[d];
-      pr[d] = ptb[d];
+      t.kr[d] = a.ktab[d];
+      t.rr[d] = a.rtab[d];
+      t.pr[d] = a.ptab[d];
     }
-    om0 = ktb[9];
+    t.om0 = a.omd[0];
   }
-  unsigned cur = 0;  // bit k set: level k's current iterate is in vb
-  auto curp = [&](int k, int o) -> T* { return ((cur >> k) & 1u) ? vb + o : va + o; };
-  auto othp = [&](int k, int o) -> T* { return ((cur >> k) & 1u) ? va + o : vb + o; };
-  auto inside = [&](int H, int N, int r) { return r >= 1 && r <= H - 2 && lane >= 1 && lane <= N - 2; };
-  auto pat = [&](const uint8_t* pk, int H, int N, int r) -> int {
-    if constexpr (MULTI) return (r >= 0 && r < H && lane < N) ? (int)pk[r * N + lane] : 0;
-    return 0;
-  };
-  auto omega = [&](int p) -> T {
-    if constexpr (MULTI) return ktb[p * kTS + 9];
-    return om0;
-  };
-  // K x at a row from rows (xm, x0, xp) and their pattern ids: DPP for the column neighbours.
-  // Must be called wave-uniformly.
-  auto Krow = [&](T xm, T x0, T xp, int qm, int q0, int qp) -> T {
-    const T xs[3] = {xm, x0, xp};
-    const int qs[3] = {qm, q0, qp};
-    T acc = 0;
-#pragma unroll
-    for (int dr = 0; dr < 3; ++dr) {
-      const T l = shr1(xs[dr], T(0)), r = shl1(xs[dr], T(0));
-      if constexpr (MULTI) {
-        const int ql = shr1(qs[dr], 0), qr = shl1(qs[dr], 0);
-        acc += ktb[ql * kTS + dr * 3 + 0] * l;
-        acc += ktb[qs[dr] * kTS + dr * 3 + 1] * xs[dr];
-        acc += ktb[qr * kTS + dr * 3 + 2] * r;
-      } else {
-        acc += kr[dr * 3 + 0] * l;
-        acc += kr[dr * 3 + 1] * xs[dr];
-        acc += kr[dr * 3 + 2] * r;
-      }
-    }
-    return acc;
-  };
-  auto block = [&](int n, int& b0, int& b1) {  // this wave's share of rows 1..n (contiguous)
-    const int per = (n + kWaves - 1) / kWaves;
-    b0 = 1 + wv * per;
-    b1 = min(n + 1, b0 + per);
-  };
-
   // ------------------------------------------------------------------ down
   int o = 0;
   for (int k = 0; k + 1 < nlev; ++k) {
-    const int H = tail_n(Ht, k), N = tail_n(Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
-    const int on = o + H * N;
-    const T* f = fs + o;
-    const uint8_t* pk = pl + o;
-    T* v = curp(k, o);
-    T* fc = fs + on;
-    int y0, y1;
-    block(H - 2, y0, y1);
-    for (int y = y0; y < y1; ++y)
-      if (inside(H, N, y)) v[y * N + lane] = omega(pat(pk, H, N, y)) * f[y * N + lane];
-    int I0, I1;
-    block(Hc - 2, I0, I1);
-    if (I0 < I1) {
-      // pre-smoothed iterate v = omd f on row y (0 off the interior), recomputed in registers
-      auto vrow = [&](int y) -> T {
-        return inside(H, N, y) ? omega(pat(pk, H, N, y)) * f[y * N + lane] : T(0);
-      };
-      auto rrow = [&](T vm, T v0, T vp, int qm, int q0, int qp, int y) -> T {
-        const T kv = Krow(vm, v0, vp, qm, q0, qp);
-        return inside(H, N, y) ? f[y * N + lane] - kv : T(0);
-      };
-      int y = 2 * I0 - 1;  // first residual row
-      T vm = vrow(y - 1), v0 = vrow(y), vp = vrow(y + 1);
-      int qm = pat(pk, H, N, y - 1), q0 = pat(pk, H, N, y), qp = pat(pk, H, N, y + 1);
-      T ra = rrow(vm, v0, vp, qm, q0, qp, y);
-      int pa = q0;
-      for (int I = I0; I < I1; ++I) {
-        // rows 2I and 2I+1 of the residual
-        vm = v0; v0 = vp; vp = vrow(2 * I + 1);
-        qm = q0; q0 = qp; qp = pat(pk, H, N, 2 * I + 1);
-        const T rb = rrow(vm, v0, vp, qm, q0, qp, 2 * I);
-        const int pb = q0;
-        vm = v0; v0 = vp; vp = vrow(2 * I + 2);
-        qm = q0; q0 = qp; qp = pat(pk, H, N, 2 * I + 2);
-        const T rc = rrow(vm, v0, vp, qm, q0, qp, 2 * I + 1);
-        const int pc = q0;
-        const T rs[3] = {ra, rb, rc};
-        const int ps[3] = {pa, pb, pc};
-        T acc = 0;
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const T l = shr1(rs[ky], T(0)), r = shl1(rs[ky], T(0));
-          if constexpr (MULTI) {
-            const int pl_ = shr1(ps[ky], 0), pr_ = shl1(ps[ky], 0);
-            acc += rtb[pl_ * kTS + ky * 3 + 0] * l;
-            acc += rtb[ps[ky] * kTS + ky * 3 + 1] * rs[ky];
-            acc += rtb[pr_ * kTS + ky * 3 + 2] * r;
-          } else {
-            acc += rr[ky * 3 + 0] * l;
-            acc += rr[ky * 3 + 1] * rs[ky];
-            acc += rr[ky * 3 + 2] * r;
-          }
-        }
-        const int J = lane >> 1;
-        if (!(lane & 1) && J >= 1 && J <= Nc - 2) fc[I * Nc + J] = a.w0 * acc;
-        ra = rc;
-        pa = pc;
-      }
-    }
-    o = on;
+    if (k == 0) t.template down<true>(k, o);
+    else t.template down<false>(k, o);
+    o += tail_n(Ht, k) * tail_n(Wt, k);
     FEA_TAIL_SYNC();
   }
   // ------------------------------------------------------------------ coarsest: 2 sweeps
-  T* const vt = a.v_t + (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1);
-  {
-    const int k = nlev - 1, H = tail_n(Ht, k), N = tail_n(Wt, k);
-    const T* f = fs + o;
-    const uint8_t* pk = pl + o;
-    auto vrow = [&](int y) -> T { return inside(H, N, y) ? omega(pat(pk, H, N, y)) * f[y * N + lane] : T(0); };
-    T* out = othp(k, o);
-    int y0, y1;
-    block(H - 2, y0, y1);
-    if (y0 < y1) {
-      T vm = vrow(y0 - 1), v0 = vrow(y0);
-      int qm = pat(pk, H, N, y0 - 1), q0 = pat(pk, H, N, y0);
-      for (int y = y0; y < y1; ++y) {
-        const T vp = vrow(y + 1);
-        const int qp = pat(pk, H, N, y + 1);
-        const T kv = Krow(vm, v0, vp, qm, q0, qp);
-        if (inside(H, N, y)) {
-          const T w = omega(q0) * (f[y * N + lane] - kv) + v0;
-          if (k == 0) vt[(long long)(y + 1) * a.ld_t + lane] = w;
-          else out[y * N + lane] = w;
-        }
-        vm = v0; v0 = vp;
-        qm = q0; q0 = qp;
-      }
-    }
-    cur ^= 1u << k;
-    if (k > 0) FEA_TAIL_SYNC();
-  }
+  t.coarsest(nlev - 1, o);
+  if (nlev > 1) FEA_TAIL_SYNC();
   // ------------------------------------------------------------------ up
   for (int k = nlev - 2; k >= 0; --k) {
-    const int H = tail_n(Ht, k), N = tail_n(Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
     const int oc = o;
-    o -= H * N;
-    const T* f = fs + o;
-    const uint8_t* pk = pl + o;
-    const uint8_t* pkc = pl + oc;
-    T* v = curp(k, o);
-    const T* e = curp(k + 1, oc);
-    T* out = othp(k, o);
-    int y0, y1;
-    block(H - 2, y0, y1);
-    // (a) v += w1 P e on this wave's rows, in place (the general path's prolong_add, same order)
-    for (int y = y0; y < y1; ++y) {
-      if (!inside(H, N, y)) continue;
-      T acc = 0;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int cy = y + 1 - ky;
-        if (cy & 1) continue;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int cx = lane + 1 - kx;
-          if (cx & 1) continue;
-          const int I = cy >> 1, J = cx >> 1;
-          const bool ein = I >= 1 && I <= Hc - 2 && J >= 1 && J <= Nc - 2;
-          const int j = I * Nc + J;
-          const T ev = ein ? e[j] : T(0);
-          if constexpr (MULTI) acc += ptb[(int)pkc[j] * kTS + ky * 3 + kx] * ev;
-          else acc += pr[ky * 3 + kx] * ev;
-        }
-      }
-      v[y * N + lane] += a.w1 * acc;
-    }
-    FEA_TAIL_SYNC();
-    // (b) one sweep from the corrected iterate (rows from LDS, columns by DPP)
-    auto xrow = [&](int y) -> T { return inside(H, N, y) ? v[y * N + lane] : T(0); };
-    if (y0 < y1) {
-      T xm = xrow(y0 - 1), x0 = xrow(y0);
-      int qm = pat(pk, H, N, y0 - 1), q0 = pat(pk, H, N, y0);
-      for (int y = y0; y < y1; ++y) {
-        const T xp = xrow(y + 1);
-        const int qp = pat(pk, H, N, y + 1);
-        const T kx_ = Krow(xm, x0, xp, qm, q0, qp);
-        if (inside(H, N, y)) {
-          const T w = omega(q0) * (f[y * N + lane] - kx_) + x0;
-          if (k == 0) vt[(long long)(y + 1) * a.ld_t + lane] = w;
-          else out[y * N + lane] = w;
-        }
-        xm = x0; x0 = xp;
-        qm = q0; q0 = qp;
-      }
-    }
-    cur ^= 1u << k;
+    o -= tail_n(Ht, k) * tail_n(Wt, k);
+    t.up(k, o, oc);
     if (k > 0) FEA_TAIL_SYNC();
   }
 }
@@ -351,15 +424,18 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
       if (r < Ht && lane == 0 && Wt == 65) fs[r * Wt + 64] = b64[i];
     }
   }
-  FEA_TAIL_SYNC();
   if (fast) {
-    tail_fast<T, MULTI>(a, va, vb, fs, ktb, rtb, ptb, pl, wv, lane
+    // single pattern: the first down phase reads f_t from HBM itself and the tables come from
+    // uniform loads, so the staging only has to land before the up phase (later barriers cover it)
+    if (MULTI || nlev == 1) FEA_TAIL_SYNC();
+    tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
 #ifdef FEA_TAIL_TRACE
                         , nph
 #endif
     );
     return;
   }
+  FEA_TAIL_SYNC();
 
   // pattern offset (into a stride-10 table) of node j of a level whose map starts at pk
   auto P = [&](const uint8_t* pk, int j) -> int { return MULTI ? pk[j] * kTS : 0; };

@@ -31,20 +31,36 @@ def needs_build():
 
 
 def build(force=False, verbose=True, out=None, defines=()):
-    """out / defines: A/B variant libraries for tools/ (loaded with FEANET_LIB_OVERRIDE)."""
+    """out / defines: A/B variant libraries for tools/ (loaded with FEANET_LIB_OVERRIDE).
+    Each source compiles to its own object in parallel (no device code crosses translation units),
+    then one link step."""
     if out is None and not force and not needs_build():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
     target = out or LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objdir = target + ".objs"
+    os.makedirs(objdir, exist_ok=True)
     # -ffp-contract=on: a*b+c is fused only within one source expression, so a value recomputed
     # at a different call site (task-edge rows, edge lanes) rounds identically -> results are
     # independent of rows-per-task and batch size (bitwise)
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-ffp-contract=on", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-pass-failed", *[f"-D{d}" for d in defines], f"-I{INCLUDE}", f"-I{CSRC}", *sources(),
-           "-o", target + ".tmp"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-ffp-contract=on", "-std=c++17", "-fPIC", "-Wno-pass-failed",
+             *[f"-D{d}" for d in defines], f"-I{INCLUDE}", f"-I{CSRC}"]
+    objs = []
+    cmds = []
+    for src in sources():
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmds.append([hipcc, *flags, "-c", src, "-o", obj])
     if verbose:
-        print("[feanet_amd.build]", " ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+        print("[feanet_amd.build]", " ".join(cmds[0][:-4]), "-c <each of", len(cmds), "sources>", file=sys.stderr)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        for c, r in zip(cmds, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds)):
+            if r.returncode != 0:
+                sys.stderr.write(r.stdout + r.stderr)
+                raise subprocess.CalledProcessError(r.returncode, c)
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", target + ".tmp"], check=True)
     os.replace(target + ".tmp", target)
     return target
 
