@@ -165,18 +165,16 @@ struct TailFast {
     }
   }
 
-  // level k (offset o) -> f_{k+1}; GLOBAL: f_k is f_t in HBM (level 0)
-  template <bool GLOBAL>
-  __device__ __forceinline__ void down(int k, int o) const {
-    constexpr int kWaves = kTailThreads / 64;
-    constexpr int R = 2 * kTailDownRows + 3;
+  // level k (offset o) -> f_{k+1}; PER coarse rows per wave.  GLOBAL: f_k is f_t in HBM (level 0);
+  // the wave then also writes the rows it loaded into LDS for the up phase (overlapping rows of
+  // neighbouring waves are written twice with the same value), which replaces a separate staging pass.
+  template <bool GLOBAL, int PER>
+  __device__ __forceinline__ void down_rows(int k, int o, int I0, int I1) const {
+    constexpr int R = 2 * PER + 3;
     const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
-    const T* f = fs + o;
+    T* f = fs + o;
     const uint8_t* pk = pl + o;
     T* fc = fs + o + H * N;
-    const int per = (Hc - 2 + kWaves - 1) / kWaves;
-    const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
-    if (I0 >= I1) return;  // wave-uniform
     const int yb = 2 * I0 - 2;  // rows yb .. yb + R - 1 (residual rows yb + 1 .. yb + R - 2)
     T fr[R], v[R], vl[R], vr[R], r[R], rl[R], rrt[R];
     int q[R], ql[R], qr[R];
@@ -186,6 +184,11 @@ struct TailFast {
       if constexpr (GLOBAL) fr[j] = fg[(long long)y * ld + lane];
       else fr[j] = f[y * N + lane];
       q[j] = pat(pk, H, N, yb + j);
+    }
+    if constexpr (GLOBAL) {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (yb + j < H && lane < N) f[(yb + j) * N + lane] = fr[j];
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) v[j] = inside(H, N, yb + j) ? omega(q[j]) * fr[j] : T(0);
@@ -201,7 +204,7 @@ struct TailFast {
     const int J = lane >> 1;
     const bool st = !(lane & 1) && J >= 1 && J <= Nc - 2;
 #pragma unroll
-    for (int i = 0; i < kTailDownRows; ++i) {
+    for (int i = 0; i < PER; ++i) {
       if (I0 + i >= I1) break;
       T acc = 0;
 #pragma unroll
@@ -215,17 +218,24 @@ struct TailFast {
       if (st) fc[(I0 + i) * Nc + J] = a.w0 * acc;
     }
   }
-
-  // coarsest level k: v1 = omd f, v2 = v1 + omd (f - K v1)
-  __device__ __forceinline__ void coarsest(int k, int o) const {
+  template <bool GLOBAL>
+  __device__ __forceinline__ void down(int k, int o) const {
     constexpr int kWaves = kTailThreads / 64;
-    constexpr int R = kTailUpRows + 2;
+    const int Hc = (tail_n(a.Ht, k) + 1) / 2;
+    const int per = (Hc - 2 + kWaves - 1) / kWaves;  // <= kTailDownRows
+    const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
+    if (I0 >= I1) return;  // wave-uniform
+    if (per == 1) down_rows<GLOBAL, 1>(k, o, I0, I1);
+    else down_rows<GLOBAL, kTailDownRows>(k, o, I0, I1);
+  }
+
+  // coarsest level k: v1 = omd f, v2 = v1 + omd (f - K v1); PER rows per wave
+  template <int PER>
+  __device__ __forceinline__ void coarsest_rows(int k, int o, int y0, int y1) const {
+    constexpr int R = PER + 2;
     const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k);
     const T* f = fs + o;
     const uint8_t* pk = pl + o;
-    const int per = (H - 2 + kWaves - 1) / kWaves;
-    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
-    if (y0 >= y1) return;
     const int yb = y0 - 1;
     T fr[R], v[R], vl[R], vr[R];
     int q[R], ql[R], qr[R];
@@ -252,10 +262,11 @@ struct TailFast {
   }
 
   // level k (offset o) from the correction of level k + 1 (offset oc): x = omd f + w1 P e, one sweep.
-  // PAR = parity of the wave's first window row, so every coarse-row index is a compile-time constant.
-  template <int PAR>
+  // PAR = parity of the wave's first window row, so every coarse-row index is a compile-time constant;
+  // PER rows per wave.
+  template <int PAR, int PER>
   __device__ __forceinline__ void up_rows(int k, int o, int oc, int y0, int y1) const {
-    constexpr int R = kTailUpRows + 2;        // x rows y0-1 .. y0+R-2
+    constexpr int R = PER + 2;                // x rows y0-1 .. y0+R-2
     constexpr int C = (PAR + R) / 2 + 1;      // coarse rows Ib .. Ib+C-1 that they touch
     const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
     const T* f = fs + o;
@@ -320,14 +331,37 @@ struct TailFast {
     }
   }
 
+  // rows 1 .. H-2 of level k over the 16 waves: dispatch on the rows per wave (<= kTailUpRows)
+  template <int PAR>
+  __device__ __forceinline__ void up_par(int k, int o, int oc, int per, int y0, int y1) const {
+    switch (per) {
+      case 1: up_rows<PAR, 1>(k, o, oc, y0, y1); break;
+      case 2: up_rows<PAR, 2>(k, o, oc, y0, y1); break;
+      case 3: up_rows<PAR, 3>(k, o, oc, y0, y1); break;
+      default: up_rows<PAR, kTailUpRows>(k, o, oc, y0, y1); break;
+    }
+  }
   __device__ __forceinline__ void up(int k, int o, int oc) const {
     constexpr int kWaves = kTailThreads / 64;
     const int H = tail_n(a.Ht, k);
     const int per = (H - 2 + kWaves - 1) / kWaves;
     const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
     if (y0 >= y1) return;
-    if ((y0 - 1) & 1) up_rows<1>(k, o, oc, y0, y1);
-    else up_rows<0>(k, o, oc, y0, y1);
+    if ((y0 - 1) & 1) up_par<1>(k, o, oc, per, y0, y1);
+    else up_par<0>(k, o, oc, per, y0, y1);
+  }
+  __device__ __forceinline__ void coarsest(int k, int o) const {
+    constexpr int kWaves = kTailThreads / 64;
+    const int H = tail_n(a.Ht, k);
+    const int per = (H - 2 + kWaves - 1) / kWaves;
+    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+    if (y0 >= y1) return;
+    switch (per) {
+      case 1: coarsest_rows<1>(k, o, y0, y1); break;
+      case 2: coarsest_rows<2>(k, o, y0, y1); break;
+      case 3: coarsest_rows<3>(k, o, y0, y1); break;
+      default: coarsest_rows<kTailUpRows>(k, o, y0, y1); break;
+    }
   }
 };
 
@@ -390,23 +424,25 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
 
   // V(1,1) (the default MultiGrid.Step / iterate schedule) runs the fused row-wave path below; it
   // masks every read outside a level's interior, so only the general path needs zeroed buffers
-  const bool fast = a.nu1 == 1 && a.nu2 == 1 && !a.q2;
-  if (!fast) {
+  if (!(a.nu1 == 1 && a.nu2 == 1 && !a.q2)) {
     for (int i = tid; i < 3 * tot; i += kTailThreads) va[i] = T(0);
     FEA_TAIL_SYNC();  // the zero fill must land before f_t is staged into the same region
   }
-  const int nt = MULTI ? a.ntab : 1;
-  for (int i = tid; i < nt * kTS; i += kTailThreads) {
-    const int p = i / kTS, d = i - p * kTS;
-    ktb[i] = d == 9 ? a.omd[p] : a.ktab[p * 9 + d];
-    rtb[i] = d == 9 ? T(0) : a.rtab[p * 9 + d];
-    ptb[i] = d == 9 ? T(0) : a.ptab[p * 9 + d];
+  const bool fast = a.nu1 == 1 && a.nu2 == 1 && !a.q2;
+  if (MULTI || !fast) {  // (the single-pattern fast path keeps its tables in registers)
+    const int nt = MULTI ? a.ntab : 1;
+    for (int i = tid; i < nt * kTS; i += kTailThreads) {
+      const int p = i / kTS, d = i - p * kTS;
+      ktb[i] = d == 9 ? a.omd[p] : a.ktab[p * 9 + d];
+      rtb[i] = d == 9 ? T(0) : a.rtab[p * 9 + d];
+      ptb[i] = d == 9 ? T(0) : a.ptab[p * 9 + d];
+    }
   }
   if constexpr (MULTI)
     for (int i = tid; i < tot; i += kTailThreads) pl[i] = a.pid[i];
   const int wv = tid >> 6, lane = tid & 63;  // wave = row group, lane = column (Wt <= 65)
   constexpr int kWaves = kTailThreads / 64;
-  {
+  if (!fast || nlev == 1) {
     const T* src = a.f_t + (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1);
     constexpr int kRows = (kTailMaxN + kWaves - 1) / kWaves;  // rows per wave, all loads in flight at once
     T buf[kRows], b64[kRows];
@@ -425,8 +461,8 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     }
   }
   if (fast) {
-    // single pattern: the first down phase reads f_t from HBM itself and the tables come from
-    // uniform loads, so the staging only has to land before the up phase (later barriers cover it)
+    // the first down phase reads f_t from HBM itself and stages it for the up phase; single pattern:
+    // the tables come from uniform loads, so nothing has to land before it
     if (MULTI || nlev == 1) FEA_TAIL_SYNC();
     tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
 #ifdef FEA_TAIL_TRACE
