@@ -252,29 +252,32 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
     P[j] = q;
     if constexpr (MULTI) q += (g[j].nr * g[j].nc + 15) / 16 * 16;
   }
-  const TabLoad<T> tl = tables_issue<T>(a.ktab, a.omd, a.xtab, a.ntab, a.nx);
-  {
-    const StageJob<T> jf[1] = {{a.f[0] + (long long)b * a.bs[0], F[0], g[0], a.H[0], a.W[0], a.ld[0], OFF}};
-    if constexpr (MULTI) {
-      StageJob<uint8_t> jp[k];
-#pragma unroll
-      for (int j = 0; j < k; ++j) jp[j] = {a.pid[j], P[j], g[j], a.H[j], a.W[j], a.ld[j], OFF};
-      stage_batch<uint8_t, k>(jp);
-    }
-    stage_batch<T, 1>(jf);
-  }
-  tables_commit<T>(tl, ktb, xtb, a.ntab, a.nx);
-  FEA_MID_SYNC(0);
+  // single pattern: weights in registers from uniform loads and the top level read straight from
+  // HBM by the first phase (no staging pass, nothing to wait for before it); two materials: tables
+  // and the pattern maps of every level go through LDS first
   T ks[9], rs[9], om = T(0);
-  if constexpr (!MULTI) {
+  if constexpr (MULTI) {
+    const TabLoad<T> tl = tables_issue<T>(a.ktab, a.omd, a.xtab, a.ntab, a.nx);
+    StageJob<uint8_t> jp[k];
+#pragma unroll
+    for (int j = 0; j < k; ++j) jp[j] = {a.pid[j], P[j], g[j], a.H[j], a.W[j], a.ld[j], OFF};
+    stage_batch<uint8_t, k>(jp);
+    tables_commit<T>(tl, ktb, xtb, a.ntab, a.nx);
+    FEA_MID_SYNC(0);
+  } else {
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-      ks[d] = ktb[d];
-      rs[d] = xtb[d];
+      ks[d] = a.ktab[d];
+      rs[d] = a.xtab[d];
     }
-    om = ktb[9];
+    om = a.omd[0];
   }
 
+  // Per level: wave w owns a contiguous block of coarse-region rows; for each chunk of <= 2 of them it
+  // loads the 2 PER + 3 fine-region rows they depend on at once (LDS, or HBM on the top level),
+  // forms v = omd f, the residual rows r = f - K v and their restriction in registers (column
+  // neighbours by DPP, each row shifted once), so a level costs one barrier and one load round trip.
+  // Per-node expressions and their order are those of k_mg_resid_restrict (zero-guess mode).
   constexpr int NW = kMidThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -283,100 +286,129 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
     const int H = a.H[j], W = a.W[j], Hc = a.H[j + 1], Wc = a.W[j + 1];
     const T* f = F[j];
     const uint8_t* pj = P[j];
-    // row-wave form (regions are <= 64 columns): lane = column G.c0 + lane, x-neighbours by DPP
+    // row-wave form (regions are <= 64 columns): lane = column G.c0 + lane
     const int c = G.c0 + lane;
     const bool lv = lane < G.nc;
     const bool cin = lv && c >= 1 && c <= W - 2;
-    // (1) residual rows of the region shrunk by one: r = f - K v, v = omd f inside
-    //     (k_mg_resid_restrict zero-guess mode; kapply order: rows y-1, y, y+1, columns left to right)
-    const int rn = G.nr - 2;
-    for (int yr = wv; yr < rn; yr += NW) {
-      const int y = G.r0 + 1 + yr;
-      T fr[3], vr[3];
-      int pr[3] = {0, 0, 0};
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const int yy = yr + d, i = yy * G.nc + lane;
-        fr[d] = lv ? f[i] : T(0);
-        if constexpr (MULTI) pr[d] = lv ? (int)pj[i] : 0;
-        const int yd = y + d - 1;
-        const bool in = cin && yd >= 1 && yd <= H - 2;
-        T om_ = om;
-        if constexpr (MULTI) om_ = ktb[pr[d] * kMS + 9];
-        vr[d] = in ? om_ * fr[d] : T(0);
-      }
-      T acc;
-      if constexpr (!MULTI) {
-        acc = ks[0] * shr1(vr[0], T(0));
-        acc += ks[1] * vr[0];
-        acc += ks[2] * shl1(vr[0], T(0));
-        acc += ks[3] * shr1(vr[1], T(0));
-        acc += ks[4] * vr[1];
-        acc += ks[5] * shl1(vr[1], T(0));
-        acc += ks[6] * shr1(vr[2], T(0));
-        acc += ks[7] * vr[2];
-        acc += ks[8] * shl1(vr[2], T(0));
-      } else {
-        const int l0 = shr1(pr[0], 0), r0 = shl1(pr[0], 0), l1 = shr1(pr[1], 0), r1 = shl1(pr[1], 0);
-        const int l2 = shr1(pr[2], 0), r2 = shl1(pr[2], 0);
-        acc = ktb[l0 * kMS + 0] * shr1(vr[0], T(0));
-        acc += ktb[pr[0] * kMS + 1] * vr[0];
-        acc += ktb[r0 * kMS + 2] * shl1(vr[0], T(0));
-        acc += ktb[l1 * kMS + 3] * shr1(vr[1], T(0));
-        acc += ktb[pr[1] * kMS + 4] * vr[1];
-        acc += ktb[r1 * kMS + 5] * shl1(vr[1], T(0));
-        acc += ktb[l2 * kMS + 6] * shr1(vr[2], T(0));
-        acc += ktb[pr[2] * kMS + 7] * vr[2];
-        acc += ktb[r2 * kMS + 8] * shl1(vr[2], T(0));
-      }
-      const bool in = cin && y >= 1 && y <= H - 2;
-      if (lv) Rs[yr * G.nc + lane] = in ? fr[1] - acc : T(0);
-    }
-    FEA_MID_SYNC(1 + 2 * j);
-    // (2) restriction into the next level's region: even lane 2 + 2 JJ holds fine column 2J
+    const T* src = a.f[0] + (long long)b * a.bs[0] + OFF + min(max(c, 0), W - 1);  // top level, row -1
+    const int ld0 = a.ld[0];
     T* fc = F[j + 1];
     T* go = a.fo[j + 1] + (long long)b * a.bs[j + 1];
     const int ldc = a.ld[j + 1];
-    const int JJ = (lane - 2) >> 1;
+    const int JJ = (lane - 2) >> 1;  // even lane 2 + 2 JJ holds fine column 2J
     const int J = C.c0 + JJ;
     const bool outl = !(lane & 1) && lane >= 2 && JJ < C.nc;
-    for (int II = wv; II < C.nr; II += NW) {
-      const int I = C.r0 + II;
-      const int ry = 2 * I - 1 - (G.r0 + 1);  // Rs row of fine row 2I-1
-      T acc = T(0);
-      bool first = true;
+    const bool jin = J >= 1 && J <= Wc - 2, jown = J >= os_c[j + 1] && J < oe_c[j + 1];
+    auto rows = [&](auto per_c, auto glob_c, int II0, int II1) {
+      constexpr int PER = decltype(per_c)::value;
+      constexpr bool GLOB = decltype(glob_c)::value;
+      constexpr int R = 2 * PER + 3;  // fine-region rows 2 II0 .. 2 II0 + R - 1
+      T fr[R], v[R], vl[R], vh[R], r[R], rl[R], rh[R];
+      int pr[R], pl[R], ph[R];
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int i = (ry + ky) * G.nc + lane;
-        const T rr = lv ? Rs[i] : T(0);
-        const T rl = shr1(rr, T(0)), rh = shl1(rr, T(0));
-        if constexpr (!MULTI) {
-          if (first) acc = rs[ky * 3 + 0] * rl;
-          else acc += rs[ky * 3 + 0] * rl;
-          acc += rs[ky * 3 + 1] * rr;
-          acc += rs[ky * 3 + 2] * rh;
-        } else {
-          // pattern of the fine node (2I-1+ky, 2J-1+dx): region row ry+ky+1
-          const int q = lv ? (int)pj[(ry + ky + 1) * G.nc + lane] : 0;
-          const int ql = shr1(q, 0), qh = shl1(q, 0);
-          if (first) acc = xtb[ql * kMS + ky * 3 + 0] * rl;
-          else acc += xtb[ql * kMS + ky * 3 + 0] * rl;
-          acc += xtb[q * kMS + ky * 3 + 1] * rr;
-          acc += xtb[qh * kMS + ky * 3 + 2] * rh;
+      for (int d = 0; d < R; ++d) {
+        const int rr = 2 * II0 + d, y = G.r0 + rr;
+        if constexpr (GLOB) fr[d] = src[(long long)(min(max(y, 0), H - 1) + 1) * ld0];
+        else fr[d] = f[min(rr, G.nr - 1) * G.nc + lane];
+        pr[d] = 0;
+        if constexpr (MULTI) {
+          const int pv = pj[min(rr, G.nr - 1) * G.nc + min(lane, G.nc - 1)];
+          pr[d] = lv ? pv : 0;
         }
-        first = false;
       }
-      if (outl) {
-        T o = T(0);
-        if (I >= 1 && I <= Hc - 2 && J >= 1 && J <= Wc - 2) {
-          o = a.w * acc;
-          if (I >= os_r[j + 1] && I < oe_r[j + 1] && J >= os_c[j + 1] && J < oe_c[j + 1])
-            go[(long long)(I + 1) * ldc + OFF + J] = o;
+#pragma unroll
+      for (int d = 0; d < R; ++d) {
+        const int y = G.r0 + 2 * II0 + d;
+        const bool in = cin && y >= 1 && y <= H - 2;
+        T om_ = om;
+        if constexpr (MULTI) om_ = ktb[pr[d] * kMS + 9];
+        v[d] = in ? om_ * fr[d] : T(0);
+        vl[d] = shr1z(v[d]);
+        vh[d] = shl1z(v[d]);
+        pl[d] = ph[d] = 0;
+        if constexpr (MULTI) {
+          pl[d] = shr1z(pr[d]);
+          ph[d] = shl1z(pr[d]);
         }
-        fc[II * C.nc + JJ] = o;
+      }
+      r[0] = r[R - 1] = T(0);
+#pragma unroll
+      for (int d = 1; d < R - 1; ++d) {
+        // (1) residual row: kapply order, rows d-1, d, d+1, columns left to right
+        T acc;
+        if constexpr (!MULTI) {
+          acc = ks[0] * vl[d - 1];
+          acc += ks[1] * v[d - 1];
+          acc += ks[2] * vh[d - 1];
+          acc += ks[3] * vl[d];
+          acc += ks[4] * v[d];
+          acc += ks[5] * vh[d];
+          acc += ks[6] * vl[d + 1];
+          acc += ks[7] * v[d + 1];
+          acc += ks[8] * vh[d + 1];
+        } else {
+          acc = ktb[pl[d - 1] * kMS + 0] * vl[d - 1];
+          acc += ktb[pr[d - 1] * kMS + 1] * v[d - 1];
+          acc += ktb[ph[d - 1] * kMS + 2] * vh[d - 1];
+          acc += ktb[pl[d] * kMS + 3] * vl[d];
+          acc += ktb[pr[d] * kMS + 4] * v[d];
+          acc += ktb[ph[d] * kMS + 5] * vh[d];
+          acc += ktb[pl[d + 1] * kMS + 6] * vl[d + 1];
+          acc += ktb[pr[d + 1] * kMS + 7] * v[d + 1];
+          acc += ktb[ph[d + 1] * kMS + 8] * vh[d + 1];
+        }
+        acc = keep(acc);
+        const int y = G.r0 + 2 * II0 + d;
+        const bool in = cin && y >= 1 && y <= H - 2;
+        r[d] = in ? fr[d] - acc : T(0);
+        rl[d] = shr1z(r[d]);
+        rh[d] = shl1z(r[d]);
+      }
+      // (2) restriction of coarse rows II0 + i: residual rows 2i+1 .. 2i+3 of the window
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        if (II0 + i >= II1) break;
+        T acc = T(0);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int d = 2 * i + 1 + ky;
+          if constexpr (!MULTI) {
+            if (ky == 0) acc = rs[0] * rl[d];
+            else acc += rs[ky * 3 + 0] * rl[d];
+            acc += rs[ky * 3 + 1] * r[d];
+            acc += rs[ky * 3 + 2] * rh[d];
+          } else {
+            if (ky == 0) acc = xtb[pl[d] * kMS + 0] * rl[d];
+            else acc += xtb[pl[d] * kMS + ky * 3 + 0] * rl[d];
+            acc += xtb[pr[d] * kMS + ky * 3 + 1] * r[d];
+            acc += xtb[ph[d] * kMS + ky * 3 + 2] * rh[d];
+          }
+        }
+        acc = keep(acc);
+        const int II = II0 + i, I = C.r0 + II;
+        if (outl) {
+          T o = T(0);
+          if (I >= 1 && I <= Hc - 2 && jin) {
+            o = a.w * acc;
+            if (I >= os_r[j + 1] && I < oe_r[j + 1] && jown) go[(long long)(I + 1) * ldc + OFF + J] = o;
+          }
+          fc[II * C.nc + JJ] = o;
+        }
+      }
+    };
+    const int per = (C.nr + NW - 1) / NW;
+    const int II0 = wv * per, II1 = min(C.nr, II0 + per);
+    for (int s0 = II0; s0 < II1; s0 += 2) {  // wave-uniform chunks of <= 2 coarse rows
+      const int s1 = min(s0 + 2, II1);
+      if (s1 - s0 == 2) {
+        if (j == 0) rows(std::integral_constant<int, 2>{}, std::true_type{}, s0, s1);
+        else rows(std::integral_constant<int, 2>{}, std::false_type{}, s0, s1);
+      } else {
+        if (j == 0) rows(std::integral_constant<int, 1>{}, std::true_type{}, s0, s1);
+        else rows(std::integral_constant<int, 1>{}, std::false_type{}, s0, s1);
       }
     }
-    FEA_MID_SYNC(2 + 2 * j);
+    if (j + 1 < k) FEA_MID_SYNC(1 + j);
   }
   FEA_MID_MARK(2 * blockIdx.x + 1);
 }
@@ -459,6 +491,11 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
     om = ktb[9];
   }
 
+  // Per level: wave w owns a contiguous block of u-region rows; for each chunk of <= 4 of them it forms
+  // the corrected iterate x = v + w1 P(e) on the chunk's rows plus one halo row on each side (every
+  // LDS load of the chunk issued up front), then the sweep u = x + omd (f - K x) — one barrier per
+  // level (the halo rows of x are recomputed by both neighbouring waves, bitwise the same values).
+  // Per-node expressions and their order are those of k_mg_prolong (ZU mode).
   constexpr int NW = kMidThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -482,103 +519,148 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
     const int iL = min(max(cL - C.c0, 0), C.nc - 1), iR = min(max(cR - C.c0, 0), C.nc - 1);
     const int qL = min(max(cL - PC.c0, 0), PC.nc - 1), qR = min(max(cR - PC.c0, 0), PC.nc - 1);
     const bool codd = (c & 1) != 0;
-    // (1) x = v + w1 P(e) on the x region (k_mg_prolong: correct_even / correct_odd, crow_term)
-    auto term = [&](int I, int ky) -> T {
-      const T eL = e[(I - C.r0) * C.nc + iL], eR = e[(I - C.r0) * C.nc + iR];
-      T wl = T(0), wm = T(0), wr = T(0);
-      if constexpr (MULTI) {
-        const int pL = pc[(I - PC.r0) * PC.nc + qL], pR = pc[(I - PC.r0) * PC.nc + qR];
-        wl = xtb[pL * kMS + ky * 3 + 2];
-        wr = xtb[pR * kMS + ky * 3 + 0];
-        wm = xtb[pR * kMS + ky * 3 + 1];
-      } else {
-        wl = ps[ky * 3 + 2];
-        wr = ps[ky * 3 + 0];
-        wm = ps[ky * 3 + 1];
-      }
-      T tt;
-      if (codd) {
-        tt = wl * eL;
-        tt += wr * eR;
-      } else {
-        tt = wm * eR;
-      }
-      return tt;
-    };
-    for (int yy = wv; yy < x.nr; yy += NW) {
-      const int y = x.r0 + yy;
-      T xv = T(0);
-      if (y >= 0 && y < H) {  // wave-uniform
-        const int i = yy * x.nc + lane;
-        T v = T(0);
-        if (cin && y >= 1 && y <= H - 2) {
-          if constexpr (MULTI) v = ktb[pj[i] * kMS + 9] * f[i];
-          else v = om * f[i];
-        }
-        if ((y & 1) == 0) {
-          v += a.w * term(y >> 1, 1);
-        } else {
-          const T tt = term((y - 1) >> 1, 2) + term((y + 1) >> 1, 0);
-          v += a.w * tt;
-        }
-        xv = cing ? v : T(0);
-      }
-      if (lv) X[yy * x.nc + lane] = xv;
-    }
-    FEA_MID_SYNC(1 + 2 * (k - 1 - j));
-    // (2) u = x + omd (f - K x) on the u region (interior), 0 on boundary nodes
     const Reg U0 = u[j];
     T* un = j > 0 ? U[j] : nullptr;
     T* go = j == 0 ? a.out + (long long)b * a.bs[0] : nullptr;
     const bool lo = lane >= 1 && lane <= U0.nc;  // u-region column c = U0.c0 + lane - 1
-    for (int yy = wv; yy < U0.nr; yy += NW) {
-      const int y = U0.r0 + yy;
-      T xr[3];
-      int pr[3] = {0, 0, 0};
+    auto rows = [&](auto par_c, auto per_c, int yy0, int yy1) {
+      constexpr int PAR = decltype(par_c)::value;  // parity of the first x row's grid row
+      constexpr int PER = decltype(per_c)::value;
+      constexpr int R = PER + 2;                   // x-region rows yy0 .. yy0 + R - 1
+      constexpr int NC = (PAR + R) / 2 + 1;        // coarse rows Ib .. Ib + NC - 1 they read
+      const int yf = x.r0 + yy0, Ib = yf >> 1;     // yf = 2 Ib + PAR
+      T fr[R], eL[NC], eR[NC];
+      int pr[R], pL[NC], pR[NC];
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const int i = (yy + d) * x.nc + lane;
-        xr[d] = lv ? X[i] : T(0);
-        if constexpr (MULTI) pr[d] = lv ? (int)pj[i] : 0;
-      }
-      const int i1 = (yy + 1) * x.nc + lane;
-      T acc;
-      if constexpr (!MULTI) {
-        acc = ks[0] * shr1(xr[0], T(0));
-        acc += ks[1] * xr[0];
-        acc += ks[2] * shl1(xr[0], T(0));
-        acc += ks[3] * shr1(xr[1], T(0));
-        acc += ks[4] * xr[1];
-        acc += ks[5] * shl1(xr[1], T(0));
-        acc += ks[6] * shr1(xr[2], T(0));
-        acc += ks[7] * xr[2];
-        acc += ks[8] * shl1(xr[2], T(0));
-      } else {
-        const int l0 = shr1(pr[0], 0), r0 = shl1(pr[0], 0), l1 = shr1(pr[1], 0), r1 = shl1(pr[1], 0);
-        const int l2 = shr1(pr[2], 0), r2 = shl1(pr[2], 0);
-        acc = ktb[l0 * kMS + 0] * shr1(xr[0], T(0));
-        acc += ktb[pr[0] * kMS + 1] * xr[0];
-        acc += ktb[r0 * kMS + 2] * shl1(xr[0], T(0));
-        acc += ktb[l1 * kMS + 3] * shr1(xr[1], T(0));
-        acc += ktb[pr[1] * kMS + 4] * xr[1];
-        acc += ktb[r1 * kMS + 5] * shl1(xr[1], T(0));
-        acc += ktb[l2 * kMS + 6] * shr1(xr[2], T(0));
-        acc += ktb[pr[2] * kMS + 7] * xr[2];
-        acc += ktb[r2 * kMS + 8] * shl1(xr[2], T(0));
-      }
-      if (lo) {
-        T o = T(0);
-        if (cin && y >= 1 && y <= H - 2) {
-          const T fv = f[i1];
-          T om_ = om;
-          if constexpr (MULTI) om_ = ktb[pr[1] * kMS + 9];
-          o = om_ * (fv - acc) + xr[1];
-          if (go) go[(long long)(y + 1) * a.ld[0] + OFF + c] = o;
+      for (int d = 0; d < R; ++d) {
+        const int i = min(yy0 + d, x.nr - 1) * x.nc + lane;
+        fr[d] = f[i];
+        pr[d] = 0;
+        if constexpr (MULTI) {
+          const int pv = pj[min(yy0 + d, x.nr - 1) * x.nc + min(lane, x.nc - 1)];
+          pr[d] = lv ? pv : 0;
         }
-        if (un) un[yy * U0.nc + lane - 1] = o;
+      }
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int ci = min(max(Ib + q - C.r0, 0), C.nr - 1);
+        eL[q] = e[ci * C.nc + iL];
+        eR[q] = e[ci * C.nc + iR];
+        pL[q] = pR[q] = 0;
+        if constexpr (MULTI) {
+          const int pi = min(max(Ib + q - PC.r0, 0), PC.nr - 1);
+          pL[q] = pc[pi * PC.nc + qL];
+          pR[q] = pc[pi * PC.nc + qR];
+        }
+      }
+      // (1) x = v + w1 P(e) (k_mg_prolong: correct_even / correct_odd, crow_term)
+      auto term = [&](int q, int ky) -> T {
+        T wl, wm, wr;
+        if constexpr (MULTI) {
+          wl = xtb[pL[q] * kMS + ky * 3 + 2];
+          wr = xtb[pR[q] * kMS + ky * 3 + 0];
+          wm = xtb[pR[q] * kMS + ky * 3 + 1];
+        } else {
+          wl = ps[ky * 3 + 2];
+          wr = ps[ky * 3 + 0];
+          wm = ps[ky * 3 + 1];
+        }
+        T tt;
+        if (codd) {
+          tt = wl * eL[q];
+          tt += wr * eR[q];
+        } else {
+          tt = wm * eR[q];
+        }
+        return tt;
+      };
+      T xv[R], xl[R], xh[R];
+      int ql_[R], qh_[R];
+#pragma unroll
+      for (int d = 0; d < R; ++d) {
+        const int y = yf + d;
+        T v = T(0);
+        if (cin && y >= 1 && y <= H - 2) {
+          if constexpr (MULTI) v = ktb[pr[d] * kMS + 9] * fr[d];
+          else v = om * fr[d];
+        }
+        if (((PAR + d) & 1) == 0) {
+          v += a.w * term((PAR + d) >> 1, 1);
+        } else {
+          const T tt = term((PAR + d - 1) >> 1, 2) + term((PAR + d + 1) >> 1, 0);
+          v += a.w * tt;
+        }
+        v = keep(v);
+        xv[d] = (cing && y >= 0 && y < H) ? v : T(0);
+        xl[d] = shr1z(xv[d]);
+        xh[d] = shl1z(xv[d]);
+        ql_[d] = qh_[d] = 0;
+        if constexpr (MULTI) {
+          ql_[d] = shr1z(pr[d]);
+          qh_[d] = shl1z(pr[d]);
+        }
+      }
+      // (2) u = x + omd (f - K x) on the u rows (interior), 0 on boundary nodes
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int yy = yy0 + i;
+        if (yy >= yy1) break;
+        T acc;
+        if constexpr (!MULTI) {
+          acc = ks[0] * xl[i];
+          acc += ks[1] * xv[i];
+          acc += ks[2] * xh[i];
+          acc += ks[3] * xl[i + 1];
+          acc += ks[4] * xv[i + 1];
+          acc += ks[5] * xh[i + 1];
+          acc += ks[6] * xl[i + 2];
+          acc += ks[7] * xv[i + 2];
+          acc += ks[8] * xh[i + 2];
+        } else {
+          acc = ktb[ql_[i] * kMS + 0] * xl[i];
+          acc += ktb[pr[i] * kMS + 1] * xv[i];
+          acc += ktb[qh_[i] * kMS + 2] * xh[i];
+          acc += ktb[ql_[i + 1] * kMS + 3] * xl[i + 1];
+          acc += ktb[pr[i + 1] * kMS + 4] * xv[i + 1];
+          acc += ktb[qh_[i + 1] * kMS + 5] * xh[i + 1];
+          acc += ktb[ql_[i + 2] * kMS + 6] * xl[i + 2];
+          acc += ktb[pr[i + 2] * kMS + 7] * xv[i + 2];
+          acc += ktb[qh_[i + 2] * kMS + 8] * xh[i + 2];
+        }
+        const int y = U0.r0 + yy;
+        T om_ = om;
+        if constexpr (MULTI) om_ = ktb[pr[i + 1] * kMS + 9];
+        const T ov = keep(om_ * (fr[i + 1] - acc) + xv[i + 1]);
+        if (lo) {
+          T o = T(0);
+          if (cin && y >= 1 && y <= H - 2) {
+            o = ov;
+            if (go) go[(long long)(y + 1) * a.ld[0] + OFF + c] = o;
+          }
+          if (un) un[yy * U0.nc + lane - 1] = o;
+        }
+      }
+    };
+    auto chunk = [&](auto per_c, int s0, int s1) {
+      if ((x.r0 + s0) & 1) rows(std::integral_constant<int, 1>{}, per_c, s0, s1);
+      else rows(std::integral_constant<int, 0>{}, per_c, s0, s1);
+    };
+    const int per = (U0.nr + NW - 1) / NW;
+    const int Y0 = wv * per, Y1 = min(U0.nr, Y0 + per);
+    constexpr int CH = MULTI ? 2 : 4;  // (two materials: the pattern windows need the registers)
+    for (int s0 = Y0; s0 < Y1; s0 += CH) {  // wave-uniform chunks of <= CH u rows
+      const int n = min(CH, Y1 - s0);
+      if constexpr (CH == 4) {
+        if (n == 4) chunk(std::integral_constant<int, 4>{}, s0, s0 + 4);
+        else if (n == 3) chunk(std::integral_constant<int, 3>{}, s0, s0 + 3);
+        else if (n == 2) chunk(std::integral_constant<int, 2>{}, s0, s0 + 2);
+        else chunk(std::integral_constant<int, 1>{}, s0, s0 + 1);
+      } else {
+        if (n == 2) chunk(std::integral_constant<int, 2>{}, s0, s0 + 2);
+        else chunk(std::integral_constant<int, 1>{}, s0, s0 + 1);
       }
     }
-    FEA_MID_SYNC(2 + 2 * (k - 1 - j));
+    if (j > 0) FEA_MID_SYNC(1 + (k - 1 - j));
   }
   FEA_MID_MARK(2 * blockIdx.x + 1);
 }
