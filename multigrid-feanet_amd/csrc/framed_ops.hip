@@ -432,6 +432,13 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
 // Kernel B: fused residual + restriction (+ optional zero-guess pre-sweep).
 //   task = (strip s, coarse rows [I0, I1)), fine rows 2I0-2 .. 2I1 are read.
 // ---------------------------------------------------------------------------
+// residual + restriction: coarse-row iterations (2 fine rows each) whose loads are in flight at once
+#ifndef FEA_RR_AHEAD
+#define FEA_RR_AHEAD 2
+#endif
+constexpr int kRRAhead = FEA_RR_AHEAD;
+static_assert(kRRAhead >= 1 && kRRAhead <= 4, "residual-restriction ring of 1..4 iterations");
+
 template <typename T, bool MULTI, bool ZERO, bool NT>
 __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   using F = Frame<T>;
@@ -535,14 +542,16 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   WRow W0 = fin_w(raw_w(y0 - 1), y0 - 1);
   WRow W1 = fin_w(raw_w(y0), y0);
   WRow W2 = fin_w(raw_w(y0 + 1), y0 + 1);
-  // the fine rows of the next TWO coarse rows are in flight, in a two-slot ring indexed by the
+  // the fine rows of the next D coarse rows are in flight, in a D-slot ring indexed by the
   // iteration's parity (compile-time after the unroll below): a slot is consumed in place and
   // refilled at once, so no in-flight register is ever copied (a copy waits for its load)
-  RawW ring[2][2];
-  ring[0][0] = raw_w(2 * I0 + 1);
-  ring[0][1] = raw_w(2 * I0 + 2);
-  ring[1][0] = raw_w(2 * I0 + 3);
-  ring[1][1] = raw_w(2 * I0 + 4);
+  constexpr int D = kRRAhead;
+  RawW ring[D][2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ring[d][0] = raw_w(2 * I0 + 1 + 2 * d);
+    ring[d][1] = raw_w(2 * I0 + 2 + 2 * d);
+  }
   T Ra[V + 1], Rb[V + 1], Rc[V + 1];
   PRow<V> Pa = W1.p, Pb, Pc;
   resid(W0, W1, W2, Ra);
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     W0 = W1;
     W1 = W2;
     W2 = fin_w(ring[S][0], 2 * I + 1);
-    ring[S][0] = raw_w(2 * I + 5);
+    ring[S][0] = raw_w(2 * I + 1 + 2 * D);
     resid(W0, W1, W2, Rb);
     Pb = W1.p;
     store_v(2 * I, W1);
@@ -561,7 +570,7 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     W0 = W1;
     W1 = W2;
     W2 = fin_w(ring[S][1], 2 * I + 2);
-    ring[S][1] = raw_w(2 * I + 6);
+    ring[S][1] = raw_w(2 * I + 2 + 2 * D);
     resid(W0, W1, W2, Rc);
     Pc = W1.p;
     store_v(2 * I + 1, W1);
@@ -606,11 +615,18 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
     Pa = Pc;
   };
   int I = I0;
-  for (; I + 1 < I1; I += 2) {
+  for (; I + D - 1 < I1; I += D) {
     iter(I, std::integral_constant<int, 0>{});
-    iter(I + 1, std::integral_constant<int, 1>{});
+    if constexpr (D > 1) iter(I + 1, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 2) iter(I + 2, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 3) iter(I + 3, std::integral_constant<int, 3 % D>{});
   }
-  if (I < I1) iter(I, std::integral_constant<int, 0>{});
+  if constexpr (D > 1)
+    if (I < I1) iter(I, std::integral_constant<int, 0>{});
+  if constexpr (D > 2)
+    if (I + 1 < I1) iter(I + 1, std::integral_constant<int, 1 % D>{});
+  if constexpr (D > 3)
+    if (I + 2 < I1) iter(I + 2, std::integral_constant<int, 2 % D>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -910,6 +926,13 @@ __device__ __forceinline__ void correct_odd(Row<T, V>& u, const CRow<T, V>& ca, 
   }
 }
 
+// prolongation(+sweep): iterations (2 fine rows each) whose loads are in flight at once
+#ifndef FEA_PROLONG_AHEAD
+#define FEA_PROLONG_AHEAD 2
+#endif
+constexpr int kProlongAhead = FEA_PROLONG_AHEAD;
+static_assert(kProlongAhead >= 1 && kProlongAhead <= 4, "prolongation ring of 1..4 iterations");
+
 template <typename T, bool MULTI, bool SWEEP, bool NT, bool ZU = false>
 __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   static_assert(!ZU || SWEEP, "ZU needs the sweep's f rows");
@@ -1014,53 +1037,82 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   CRow<T, V> C0 = finish_c<T, V, MULTI>(rc(a0));
   CRow<T, V> C1 = finish_c<T, V, MULTI>(rc(a0 + 1));
   PRow<V> Pp = fp(rp(r0 - 1)), Pc = fp(rp(r0));
-  T fq[V], f0[V], f1[V];  // ZU: f's own columns of rows r0-1 (unused), r0 (f0), r0+1 (f1)
+  T fq[V], f0[V];  // ZU: f's own columns of rows r0-1 (unused), r0 (f0)
   Row<T, V> Vp = mk(ru(r0 - 1), r0 - 1, Pp, fq), Vc = mk(ru(r0), r0, Pc, f0);
   correct_even<T, V, MULTI>(Vp, C0, w1, ps, ptb);
   correct_odd<T, V, MULTI>(Vc, C0, C1, w1, ps, ptb);
-  // prefetched for the first iteration: fine rows r0+1, r0+2, coarse row a0+2, f rows r0, r0+1
-  RawRow<T, V> nU1 = ru(r0 + 1), nU2 = ru(r0 + 2);
-  RawC<T, V> nC = rc(a0 + 2);
-  RawP<V> nP1 = rp(r0 + 1), nP2 = rp(r0 + 2);
-  rf(r0, f0);
-  rf(r0 + 1, f1);
-  for (int y = r0; y < r1; y += 2) {
-    // next iteration's loads first
-    const RawRow<T, V> mU1 = ru(y + 3), mU2 = ru(y + 4);
-    const RawC<T, V> mC = rc((y + 5) / 2);
-    const RawP<V> mP1 = rp(y + 3), mP2 = rp(y + 4);
-    T g0[V], g1[V];
-    rf(y + 2, g0);
-    rf(y + 3, g1);
+  // Iteration y (odd) emits rows y and y+1 from fine rows y+1, y+2, coarse row (y+3)/2 and (not ZU)
+  // f rows y, y+1.  Those loads are in flight kProlongAhead iterations ahead, in a ring of slots
+  // indexed by the iteration's position (compile-time after the unroll below): a slot is consumed in
+  // place and refilled at once, so no in-flight register is ever copied (a copy waits for its load).
+  constexpr int D = kProlongAhead;
+  struct Slot {
+    RawRow<T, V> u1, u2;
+    RawC<T, V> c;
+    RawP<V> p1, p2;
+    T f0[V], f1[V];
+  };
+  Slot ring[D];
+  auto fill = [&](Slot& sl, int y) {
+    sl.u1 = ru(y + 1);
+    sl.u2 = ru(y + 2);
+    sl.c = rc((y + 3) / 2);
+    sl.p1 = rp(y + 1);
+    sl.p2 = rp(y + 2);
+    rf(y, sl.f0);
+    rf(y + 1, sl.f1);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) fill(ring[d], r0 + 2 * d);
+  // ZU: f's own columns of row y come from the previous iteration's window row (f0 above)
+  auto iter = [&](int y, auto slot) {
+    Slot& sl = ring[decltype(slot)::value];
+    T fa[V], fb1[V];  // f's own columns of rows y, y+1 (ZU: fb1 is filled from the window row)
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if constexpr (ZU) {
+        fa[k] = f0[k];
+      } else {
+        fa[k] = sl.f0[k];
+        fb1[k] = sl.f1[k];
+      }
+    }
     // row y+1 (even, coarse (y+1)/2 = C1)
-    const PRow<V> Pn = fp(nP1);
-    Row<T, V> Vn = mk(nU1, y + 1, Pn, f1);
+    const PRow<V> Pn = fp(sl.p1);
+    Row<T, V> Vn = mk(sl.u1, y + 1, Pn, fb1);
     correct_even<T, V, MULTI>(Vn, C1, w1, ps, ptb);
-    emit(y, Vp, Vc, Vn, Pp, Pc, Pn, f0);
+    emit(y, Vp, Vc, Vn, Pp, Pc, Pn, fa);
     if (y + 1 < r1) {
       // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
-      const CRow<T, V> C2 = finish_c<T, V, MULTI>(nC);
-      const PRow<V> Pnn = fp(nP2);
-      Row<T, V> Vnn = mk(nU2, y + 2, Pnn, g0);
+      const CRow<T, V> C2 = finish_c<T, V, MULTI>(sl.c);
+      const PRow<V> Pnn = fp(sl.p2);
+      T g0[V];
+      Row<T, V> Vnn = mk(sl.u2, y + 2, Pnn, g0);
       correct_odd<T, V, MULTI>(Vnn, C1, C2, w1, ps, ptb);
-      emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn, f1);
+      emit(y + 1, Vc, Vn, Vnn, Pc, Pn, Pnn, fb1);
       Vp = Vn;
       Vc = Vnn;
       Pp = Pn;
       Pc = Pnn;
       C1 = C2;
-    }
-    nU1 = mU1;
-    nU2 = mU2;
-    nC = mC;
-    nP1 = mP1;
-    nP2 = mP2;
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      f0[k] = g0[k];
-      if constexpr (!ZU) f1[k] = g1[k];
+      for (int k = 0; k < V; ++k) f0[k] = g0[k];
     }
+    fill(sl, y + 2 * D);
+  };
+  int y = r0;
+  for (; y + 2 * (D - 1) < r1; y += 2 * D) {
+    iter(y, std::integral_constant<int, 0>{});
+    if constexpr (D > 1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 2) iter(y + 4, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 3) iter(y + 6, std::integral_constant<int, 3 % D>{});
   }
+  if constexpr (D > 1)
+    if (y < r1) iter(y, std::integral_constant<int, 0>{});
+  if constexpr (D > 2)
+    if (y + 2 < r1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+  if constexpr (D > 3)
+    if (y + 4 < r1) iter(y + 4, std::integral_constant<int, 2 % D>{});
 }
 
 // ---------------------------------------------------------------------------
