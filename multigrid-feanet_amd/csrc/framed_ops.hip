@@ -1149,6 +1149,18 @@ static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of
 #define FEA_JOIN_NTL 1
 #endif
 constexpr bool kJoinNTL = FEA_JOIN_NTL != 0;
+// FEA_JOIN_ALT: odd row tasks stream bottom-up (see join_task).  FEA_JOIN_SHARED: the rows two tasks
+// share are loaded through the cache instead of nontemporally (with FEA_JOIN_NTL).  Same-lease A/B at
+// 4097^2 fp64 (profiles/r02_ab): ALT=1 join 82.6 us, 348 MB read per launch; ALT=0 84.3 us, 385 MB;
+// ALT=1 SHARED=1 95 us, 336 MB (the cached rows evict the right-hand side, like NTL=0).
+#ifndef FEA_JOIN_ALT
+#define FEA_JOIN_ALT 1
+#endif
+#ifndef FEA_JOIN_SHARED
+#define FEA_JOIN_SHARED 0
+#endif
+constexpr bool kJoinAlternate = FEA_JOIN_ALT != 0;
+#define REV_SHARED_LOADS (FEA_JOIN_SHARED != 0)
 
 template <typename T>
 struct Ovl3 {
@@ -1163,10 +1175,18 @@ struct Ovl3 {
 // f - K v of the post-smoothed iterate v (the end-of-cycle iterate the reference drivers measure,
 // M-FEANet-mg_test.ipynb:27428-27429) over the task's owned interior nodes — the pre-smooth of the
 // next cycle forms exactly that residual, so the norm costs no extra pass.
-template <typename T, bool MULTI, bool NT, bool NORM>
+//
+// REV: the task streams its rows bottom-up.  Odd row tasks run reversed, so two vertically adjacent
+// tasks reach the 7 rows they share (input rows each recomputes) at the same moment — both at their
+// start or both at their end — and the second read of those rows comes from the L2 (37 MB less HBM
+// traffic per launch at 4097^2 fp64, measured; nontemporal loads still allocate there).  Every node value
+// is the same expression as in the forward task: windows are passed to the stencil in grid order and
+// a coarse row's three restriction terms are summed in the forward order (ky = 0, 1, 2).
+template <typename T, bool MULTI, bool NT, bool NORM, bool REV>
 __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* rtb,
                                           const T* ptb, double& ssq) {
   constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
+  constexpr int S = REV ? -1 : 1;  // row step
   using F = Frame<T>;
   using O = Ovl3<T>;
   constexpr int V = F::VEC;
@@ -1209,21 +1229,32 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   auto crowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc) + 1) * ldc; };
   auto rc = [&](int a) { return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane); };
 
-  // ---- pipeline state (rows relative to the step's y)
-  Row<T, V> Xa{}, Xb{}, Xc{};  // x windows of rows y-2, y-1, y
-  Row<T, V> Va{}, Vb{}, Vc{};  // v windows of rows y-3, y-2, y-1
-  Row<T, V> Wa{}, Wb{}, Wc_{}; // w windows of rows y-4, y-3, y-2
-  PRow<V> P4{}, P3{}, P2{}, P1{}, P0{};  // pattern windows of rows y-4 .. y
-  T f1[V], f2[V], f3[V];       // f of rows y-1, y-2, y-3
-  T um1[V];                    // u (uncorrected) of row y-1: v keeps it on boundary nodes
-  T acc[Q];
+  // ---- pipeline state (rows relative to the step's y, s = +1 forward / -1 reversed)
+  Row<T, V> Xa{}, Xb{}, Xc{};  // x windows of rows y-2s, y-s, y
+  Row<T, V> Va{}, Vb{}, Vc{};  // v windows of rows y-3s, y-2s, y-s
+  Row<T, V> Wa{}, Wb{}, Wc_{}; // w windows of rows y-4s, y-3s, y-2s
+  PRow<V> P4{}, P3{}, P2{}, P1{}, P0{};  // pattern windows of rows y-4s .. y
+  T f1[V], f2[V], f3[V];       // f of rows y-2s, y-3s, y-4s (after the rotation at the step's end: y-s ..)
+  T um1[V];                    // u (uncorrected) of row y-s: v keeps it on boundary nodes
+  T acc[Q], t2[Q];             // forward: restriction partial sum; reversed: the ky=1 and ky=2 terms
 #pragma unroll
   for (int k = 0; k < V; ++k) f1[k] = f2[k] = f3[k] = um1[k] = T(0);
 #pragma unroll
-  for (int q = 0; q < Q; ++q) acc[q] = T(0);
+  for (int q = 0; q < Q; ++q) acc[q] = t2[q] = T(0);
 
   const int ys = 2 * I0 - 4, ye = 2 * I1 + 2;
-  // inputs u(y), f(y-1), pid(y) in flight kJoinAhead steps ahead, in a ring of buffers indexed by the
+  const int yb = REV ? ye : ys;  // first row streamed
+  // shared input rows (recomputed by the neighbouring task too) are loaded through the cache
+  auto shared_row = [&](int y) { return y <= ys + 6 || y >= ye - 6; };
+  auto load_u = [&](int y, T (&x)[V]) {
+    if constexpr (kJoinNTL && NT && REV_SHARED_LOADS) {
+      if (shared_row(y)) vload<T, V>(ub + rowo(y), x);
+      else vload<T, V, true>(ub + rowo(y), x);
+    } else {
+      vload<T, V, kJoinNTL && NT>(ub + rowo(y), x);
+    }
+  };
+  // inputs u(y), f(y-s), pid(y) in flight kJoinAhead steps ahead, in a ring of buffers indexed by the
   // step's position mod kJoinAhead (compile-time), so no in-flight register is ever copied (a copy
   // would force the wait for its load at once) — the join runs 3 waves per SIMD and needs the
   // latency cover: 4 rows x 2 KiB of u and f per wave in flight
@@ -1231,13 +1262,14 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   int pb_[kJoinAhead][V];
 #pragma unroll
   for (int q = 0; q < kJoinAhead; ++q) {
-    vload<T, V, kJoinNTL && NT>(ub + rowo(ys + q), ub_[q]);
-    vload<T, V>(fb + rowo(ys + q - 1), fb_[q]);
-    if constexpr (MULTI) pload<V>(pb + rowo(ys + q), pb_[q]);
+    load_u(yb + S * q, ub_[q]);
+    vload<T, V>(fb + rowo(yb + S * (q - 1)), fb_[q]);
+    if constexpr (MULTI) pload<V>(pb + rowo(yb + S * q), pb_[q]);
   }
-  CRow<T, V> Ca = finish_c<T, V, MULTI>(rc(ys / 2));
-  CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(ys / 2 + 1));
-  RawC<T, V> nC = rc(ys / 2 + 2);
+  // coarse rows: Ca = the row an even step uses, Cb = the next one in streaming order
+  CRow<T, V> Ca = finish_c<T, V, MULTI>(rc(yb / 2));
+  CRow<T, V> Cb = finish_c<T, V, MULTI>(rc(yb / 2 + S));
+  RawC<T, V> nC = rc(yb / 2 + 2 * S);
 
   // count: add the squared residual of the input row y to ssq (NORM; the row and lane own y)
   auto sweep_own = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
@@ -1255,10 +1287,18 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
         if (count && rin && cin[k]) ssq += (double)rr * (double)rr;
     }
   };
+  // the stencil takes its three rows in grid order (row i-1, i, i+1)
+  auto sweep3 = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
+                    const PRow<V>& pb_, const PRow<V>& pc, const T (&fy)[V], const T (&keep)[V], int y, T (&o)[V],
+                    bool count) {
+    if constexpr (REV) sweep_own(c, b, a, pc, pb_, pa, fy, keep, y, o, count);
+    else sweep_own(a, b, c, pa, pb_, pc, fy, keep, y, o, count);
+  };
 
   auto step = [&](int y, auto par) {
-    constexpr int SLOT = decltype(par)::value % kJoinAhead;  // y - ys mod kJoinAhead
-    constexpr int ODD = decltype(par)::value & 1;            // (ys is even)
+    constexpr int SLOT = decltype(par)::value % kJoinAhead;  // step index mod kJoinAhead
+    constexpr int ODD = decltype(par)::value & 1;            // y odd (yb is even)
+    const int n = REV ? ye - y : y - ys;                     // step index
     // this step's inputs; refill the slot with the rows kJoinAhead steps ahead
     T(&bu)[V] = ub_[SLOT];
     T(&bf)[V] = fb_[SLOT];
@@ -1271,9 +1311,9 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
       fy1[k] = bf[k];
       if constexpr (MULTI) p0[k] = bp[k];
     }
-    vload<T, V, kJoinNTL && NT>(ub + rowo(y + kJoinAhead), bu);
-    vload<T, V>(fb + rowo(y + kJoinAhead - 1), bf);
-    if constexpr (MULTI) pload<V>(pb + rowo(y + kJoinAhead), bp);
+    load_u(y + S * kJoinAhead, bu);
+    vload<T, V>(fb + rowo(y + S * (kJoinAhead - 1)), bf);
+    if constexpr (MULTI) pload<V>(pb + rowo(y + S * kJoinAhead), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
     T x[V];
 #pragma unroll
@@ -1281,15 +1321,17 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
       T t;
       if constexpr (!ODD) {
         t = crow_term<T, V, MULTI>(Ca, k + 1, 1, ps, ptb);
-      } else {
+      } else if constexpr (!REV) {  // coarse rows (y-1)/2 = Ca (ky = 2), (y+1)/2 = Cb (ky = 0)
         t = crow_term<T, V, MULTI>(Ca, k + 1, 2, ps, ptb) + crow_term<T, V, MULTI>(Cb, k + 1, 0, ps, ptb);
+      } else {  // coarse rows (y-1)/2 = Cb (ky = 2), (y+1)/2 = Ca (ky = 0)
+        t = crow_term<T, V, MULTI>(Cb, k + 1, 2, ps, ptb) + crow_term<T, V, MULTI>(Ca, k + 1, 0, ps, ptb);
       }
       x[k] = u0[k] + w1 * t;
     }
-    if constexpr (ODD) {  // next (even) step uses coarse row (y+1)/2 = Cb; prefetch the one after
+    if constexpr (ODD) {  // the next (even) step uses coarse row (y+s)/2 = Cb; prefetch the one after
       Ca = Cb;
       Cb = finish_c<T, V, MULTI>(nC);
-      nC = rc((y + 1) / 2 + 2);
+      nC = rc((y + S) / 2 + 2 * S);
     }
     Xa = Xb;
     Xb = Xc;
@@ -1299,30 +1341,33 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
     P2 = P1;
     P1 = P0;
     if constexpr (MULTI) P0 = own_prow<V>(p0);
-    // 2. v(y-1) = J(x) (boundary nodes keep u)
-    if (y >= ys + 2) {
+    // 2. v(y-s) = J(x) (boundary nodes keep u)
+    if (n >= 2) {
       T v[V];
-      sweep_own(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - 1, v, false);
+      sweep3(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - S, v, false);
       Va = Vb;
       Vb = Vc;
       Vc = own_row<T, V>(v);
-      // 3. w(y-2) = J(v) (boundary nodes keep v)
-      if (y >= ys + 4) {
+      // 3. w(y-2s) = J(v) (boundary nodes keep v)
+      if (n >= 4) {
         T keep[V], w[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) keep[k] = Vb.a[k + 1];
-        const int yw = y - 2;
+        const int yw = y - 2 * S;
         const bool ownr = yw >= 2 * I0 - 1 && (yw < 2 * I1 - 1 || I1 == Hc - 1) && yw <= H - 2;
-        sweep_own(Va, Vb, Vc, P3, P2, P1, f1, keep, y - 2, w, own && ownr);
+        sweep3(Va, Vb, Vc, P3, P2, P1, f1, keep, yw, w, own && ownr);
         if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, W);
         Wa = Wb;
         Wb = Wc_;
         Wc_ = own_row<T, V>(w);
-        // 4. residual row y-3 -> restriction
-        if (y >= ys + 6) {
+        // 4. residual row y-3s -> restriction
+        if (n >= 6) {
           T r[V + 1];
 #pragma unroll
-          for (int k = 0; k < V; ++k) r[k] = f2[k] - kapply<T, V, MULTI>(Wa, Wb, Wc_, P4, P3, P2, k, ks, tab);
+          for (int k = 0; k < V; ++k) {
+            if constexpr (REV) r[k] = f2[k] - kapply<T, V, MULTI>(Wc_, Wb, Wa, P2, P3, P4, k, ks, tab);
+            else r[k] = f2[k] - kapply<T, V, MULTI>(Wa, Wb, Wc_, P4, P3, P2, k, ks, tab);
+          }
           r[V] = shl1(r[0], T(0));
           auto term = [&](int q, int ky) -> T {
             T t;
@@ -1337,29 +1382,47 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
             }
             return t;
           };
-          const int yr = y - 3;
-          if constexpr (!ODD) {  // yr odd = 2I+1: ky = 2 closes coarse row I, ky = 0 opens I+1
-            if (yr > 2 * I0 - 1) {
-              const int I = (yr - 1) / 2;
-              T o[Q];
+          const int yr = y - 3 * S;
+          auto put = [&](int I, const T (&o)[Q]) {
+            if (own) {
+              T* cp = cb + (long long)(I + 1) * ldc;
+              if (J0 + Q - 1 <= Wc - 2) {
+                vstore<T, Q, kCoarseNT && NT>(cp, o);
+              } else {
 #pragma unroll
-              for (int q = 0; q < Q; ++q) o[q] = w0 * (acc[q] + term(q, 2));
-              if (own) {
-                T* cp = cb + (long long)(I + 1) * ldc;
-                if (J0 + Q - 1 <= Wc - 2) {
-                  vstore<T, Q, kCoarseNT && NT>(cp, o);
-                } else {
-#pragma unroll
-                  for (int q = 0; q < Q; ++q)
-                    if (J0 + q <= Wc - 2) cp[q] = o[q];
-                }
+                for (int q = 0; q < Q; ++q)
+                  if (J0 + q <= Wc - 2) cp[q] = o[q];
               }
             }
+          };
+          if constexpr (!REV) {
+            if constexpr (!ODD) {  // yr odd = 2I+1: ky = 2 closes coarse row I, ky = 0 opens I+1
+              if (yr > 2 * I0 - 1) {
+                T o[Q];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) acc[q] = term(q, 0);
-          } else {  // yr even = 2I: ky = 1
+                for (int q = 0; q < Q; ++q) o[q] = w0 * (acc[q] + term(q, 2));
+                put((yr - 1) / 2, o);
+              }
 #pragma unroll
-            for (int q = 0; q < Q; ++q) acc[q] = acc[q] + term(q, 1);
+              for (int q = 0; q < Q; ++q) acc[q] = term(q, 0);
+            } else {  // yr even = 2I: ky = 1
+#pragma unroll
+              for (int q = 0; q < Q; ++q) acc[q] = acc[q] + term(q, 1);
+            }
+          } else {
+            if constexpr (!ODD) {  // yr odd = 2I-1: ky = 0 closes coarse row I, ky = 2 opens I-1
+              if (yr < 2 * I1 - 1) {
+                T o[Q];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) o[q] = w0 * ((term(q, 0) + acc[q]) + t2[q]);
+                put((yr + 1) / 2, o);
+              }
+#pragma unroll
+              for (int q = 0; q < Q; ++q) t2[q] = term(q, 2);
+            } else {  // yr even = 2I: ky = 1
+#pragma unroll
+              for (int q = 0; q < Q; ++q) acc[q] = term(q, 1);
+            }
           }
         }
       }
@@ -1376,16 +1439,29 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
 
   // ye - ys + 1 steps (odd); the ring slot is a template argument, so the loop is unrolled by 4 (a
   // multiple of the ring)
-  int y = ys;
-  for (; y + 3 <= ye; y += 4) {
-    step(y, std::integral_constant<int, 0>{});
-    step(y + 1, std::integral_constant<int, 1>{});
-    step(y + 2, std::integral_constant<int, 2>{});
-    step(y + 3, std::integral_constant<int, 3>{});
+  if constexpr (!REV) {
+    int y = ys;
+    for (; y + 3 <= ye; y += 4) {
+      step(y, std::integral_constant<int, 0>{});
+      step(y + 1, std::integral_constant<int, 1>{});
+      step(y + 2, std::integral_constant<int, 2>{});
+      step(y + 3, std::integral_constant<int, 3>{});
+    }
+    if (y <= ye) step(y, std::integral_constant<int, 0>{});
+    if (y + 1 <= ye) step(y + 1, std::integral_constant<int, 1>{});
+    if (y + 2 <= ye) step(y + 2, std::integral_constant<int, 2>{});
+  } else {
+    int y = ye;
+    for (; y - 3 >= ys; y -= 4) {
+      step(y, std::integral_constant<int, 0>{});
+      step(y - 1, std::integral_constant<int, 1>{});
+      step(y - 2, std::integral_constant<int, 2>{});
+      step(y - 3, std::integral_constant<int, 3>{});
+    }
+    if (y >= ys) step(y, std::integral_constant<int, 0>{});
+    if (y - 1 >= ys) step(y - 1, std::integral_constant<int, 1>{});
+    if (y - 2 >= ys) step(y - 2, std::integral_constant<int, 2>{});
   }
-  if (y <= ye) step(y, std::integral_constant<int, 0>{});
-  if (y + 1 <= ye) step(y + 1, std::integral_constant<int, 1>{});
-  if (y + 2 <= ye) step(y + 2, std::integral_constant<int, 2>{});
 }
 
 template <typename T, bool MULTI, bool NORM, bool NT>
@@ -1404,7 +1480,10 @@ void k_mg_cycle_join(MgArgs<T> g) {
   }
   const TaskId id = decode_task(g.nstrips, g.ntr);
   double ssq = 0.0;
-  if (id.valid) join_task<T, MULTI, NT, NORM>(g, id, tab, rtb, ptb, ssq);
+  if (id.valid) {
+    if (kJoinAlternate && (id.t & 1)) join_task<T, MULTI, NT, NORM, true>(g, id, tab, rtb, ptb, ssq);
+    else join_task<T, MULTI, NT, NORM, false>(g, id, tab, rtb, ptb, ssq);
+  }
   if constexpr (NORM) norm_partial<T>(g, ssq);
 }
 
