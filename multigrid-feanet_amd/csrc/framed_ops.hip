@@ -705,7 +705,10 @@ __device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const Ta
   const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
   T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
   const int ld = g.ld;
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * lane; };
+  // lanes past the grid's last column (W - 1) load the last needed lane's columns again: the last
+  // strip of a row can be mostly outside the grid (stores are masked by column anyway)
+  const int ll = min(lane, (W - 1 - cs) / V);
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
 
   struct In {  // a raw input row: u and f own values (+ pattern ids)
     T u[V], f[V];
@@ -863,18 +866,26 @@ struct RawC {
   int ph;
 };
 
+// lq: the lane whose columns this lane loads (lane itself, or the last lane that holds a needed column
+// when the strip runs past the grid: the lanes beyond then re-read one line instead of streaming
+// columns nothing uses)
 template <typename T, int V, bool MULTI>
-__device__ __forceinline__ RawC<T, V> raw_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp, int lane) {
+__device__ __forceinline__ RawC<T, V> raw_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp, int lane,
+                                               int lq) {
   constexpr int Q = V / 2;
   RawC<T, V> c;
-  vload<T, Q>(ep + Q * lane, c.x);
+  vload<T, Q>(ep + Q * lq, c.x);
   c.h = ep[lane < 32 ? -1 : kWave * Q];
   if constexpr (MULTI) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q) c.px[q] = pp[Q * lane + q];
+    for (int q = 0; q < Q; ++q) c.px[q] = pp[Q * lq + q];
     c.ph = pp[lane < 32 ? -1 : kWave * Q];
   }
   return c;
+}
+template <typename T, int V, bool MULTI>
+__device__ __forceinline__ RawC<T, V> raw_crow(const T* __restrict__ ep, const uint8_t* __restrict__ pp, int lane) {
+  return raw_crow<T, V, MULTI>(ep, pp, lane, lane);
 }
 
 template <typename T, int V, bool MULTI>
@@ -1225,9 +1236,16 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   const uint8_t* __restrict__ pcb = MULTI ? g.pidc + cboff : nullptr;
   T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
   const int ld = g.ld, ldc = g.ldc;
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * lane; };
+  // lanes past the grid's last fine column W - 1 (coarse: Wc - 1) load the last needed lane's columns
+  // again instead of streaming columns nothing uses: the last strip of a row can be mostly outside
+  // the grid (25 % of the loaded columns at 1025 wide in fp32); stores are masked by column anyway
+  const int ll = min(lane, (W - 1 - cs) / V);
+  const int llc = min(lane, (Wc - 1 - (cs + 1) / 2) / Q);
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
   auto crowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc) + 1) * ldc; };
-  auto rc = [&](int a) { return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane); };
+  auto rc = [&](int a) {
+    return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane, llc);
+  };
 
   // ---- pipeline state (rows relative to the step's y, s = +1 forward / -1 reversed)
   Row<T, V> Xa{}, Xb{}, Xc{};  // x windows of rows y-2s, y-s, y
