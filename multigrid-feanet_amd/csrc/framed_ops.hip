@@ -269,8 +269,27 @@ __device__ __forceinline__ TaskId decode_task(int nstrips, int ntr) {
   const int rem = bid - id.b * per_b;
   id.t = rem / nsg;
   const int sg = rem - id.t * nsg;
-  id.s = sg * kWaves + (threadIdx.x >> 6);
+  id.s = sg * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform: scalar
   id.valid = id.s < nstrips;
+  return id;
+}
+
+// Linear task order for the overlapped-strip kernels (cycle join, sweep+restriction), whose strip count
+// per row is ragged (35 at 4097 wide in fp64, 5 at 1025 in fp32): a workgroup's four waves take the next
+// four (row task, strip) pairs of one sample instead of four strips of one row task, so no wave slot is
+// left empty (5 strips in two 4-wave groups idled 3 of 8 slots).  Workgroups never mix samples (the
+// fused norm partials stay per sample); only a sample's last workgroup may hold idle waves.
+__device__ __forceinline__ TaskId decode_task_lin(int nstrips, int ntr) {
+  const int per = ntr * nstrips;
+  const int wpb = (per + kWaves - 1) / kWaves;  // workgroups per sample
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  TaskId id;
+  id.b = bid / wpb;
+  // the wave index is wave-uniform: keep the task coordinates in scalar registers
+  const int w = (bid - id.b * wpb) * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  id.t = w / nstrips;
+  id.s = w - id.t * nstrips;
+  id.valid = w < per;
   return id;
 }
 
@@ -840,7 +859,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
     load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
     __syncthreads();
   }
-  const TaskId id = decode_task(g.nstrips, g.ntr);
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
   double ssq = 0.0;
   if (id.valid) sweep_restrict_task<T, MULTI, NT, NORM>(g, id, tab, rtb, ssq);
   if constexpr (NORM) norm_partial<T>(g, ssq);
@@ -1496,7 +1515,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
     load_tables<T>(ptb, g.ptab, nullptr, g.nptab, nullptr, nullptr, 0);
     __syncthreads();
   }
-  const TaskId id = decode_task(g.nstrips, g.ntr);
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
   double ssq = 0.0;
   if (id.valid) {
     if (kJoinAlternate && (id.t & 1)) join_task<T, MULTI, NT, NORM, true>(g, id, tab, rtb, ptb, ssq);
@@ -1644,12 +1663,12 @@ static int num_cus() {
 static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
   const char* e = getenv("FEANET_BALANCE");
   if ((e && atoi(e) == 0) || rows_c < 2) return rb_pow2;
-  const long long ncu = num_cus(), nsg = div_up(nstrips, kWaves);
+  const long long ncu = num_cus();
   const long long min_wg = std::max<long long>(1, target_waves() / kWaves);
   long long best_cost = -1;
   int best = rb_pow2;
   for (int rbc = 1; rbc <= rows_c && 2 * rbc <= 4 * rb_pow2; ++rbc) {
-    const long long ntr = div_up(rows_c, rbc), wgs = (long long)B * ntr * nsg;
+    const long long ntr = div_up(rows_c, rbc), wgs = (long long)B * div_up(ntr * nstrips, kWaves);  // linear order
     if (wgs < min_wg) break;  // larger tasks only lower the count further
     const long long cost = div_up(wgs, ncu) * (2 * rbc + halo);
     if (best_cost < 0 || cost < best_cost) {
@@ -1707,6 +1726,9 @@ static inline bool coarse_ok(int H, int W, int ldc, long long bsc) {
   return Hc >= 3 && Wc >= 3 && ldc >= mg_ld<T>(Wc) && ldc % Frame<T>::A == 0 && bsc >= (long long)(Hc + 2) * ldc;
 }
 
+static inline dim3 mg_grid_lin(int B, int ntr, int nstrips) {  // decode_task_lin launches
+  return dim3((unsigned)(B * div_up(ntr * nstrips, kWaves)));
+}
 static inline dim3 mg_grid(int B, int ntr, int nstrips) {
   return dim3((unsigned)(B * ntr * div_up(nstrips, kWaves)));
 }
@@ -1753,11 +1775,11 @@ extern "C" long long fea_mg_join_norm_parts(int B, int H, int W, int elem_size) 
   MgArgs<float> gf{};
   if (elem_size == 8) {
     join_config<double>(B, H, W, gd);
-    return (long long)gd.ntr * div_up(gd.nstrips, kWaves) * kWaves;
+    return (long long)div_up(gd.ntr * gd.nstrips, kWaves) * kWaves;
   }
   if (elem_size == 4) {
     join_config<float>(B, H, W, gf);
-    return (long long)gf.ntr * div_up(gf.nstrips, kWaves) * kWaves;
+    return (long long)div_up(gf.ntr * gf.nstrips, kWaves) * kWaves;
   }
   return -1;
 }
@@ -1864,7 +1886,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.rb = balanced_rb(B, g.nstrips, g.Hc - 2, 3, pick_rb(B, g.nstrips, H - 2, 2 * kRB));                    \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
     g.part = norm_ws;                                                                                        \
-    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (norm && (long long)grid.x * kWaves * 8 > (long long)fea_norm_workspace_bytes(B, H, W))               \
       return FEA_EINVAL;                                                                                     \
@@ -1943,7 +1965,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     join_config<T>(B, H, W, g);                                                                              \
     g.part = norm_ws;                                                                                        \
-    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
+    const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (norm && (long long)grid.x * kWaves * 8 > (long long)fea_norm_workspace_bytes(B, H, W))               \
       return FEA_EINVAL;                                                                                     \
