@@ -13,7 +13,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.
 tail -1 $T/smoke.log
 bash tools/profile_round.sh $TAG || exit 1
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $T/bench_steps20.json 2> $T/bench_steps20.err || { tail $T/bench_steps20.err; exit 1; }
-for cfg in "c2:--n 1024" "c3:--n 2048 --problem interface" "c5:--n 1024 --batch 256 --dtype f32" "c4one:--n 8192 --steps 200" "f32_2049:--n 2048 --dtype f32"; do
+for cfg in "c2:--n 1024 --steps 300" "c3:--n 2048 --problem interface --steps 300" "c5:--n 1024 --batch 256 --dtype f32 --steps 30 --warmup 2" "c4one:--n 8192 --steps 50" "f32_2049:--n 2048 --dtype f32 --steps 300"; do
   name=${cfg%%:*}; args=${cfg#*:}
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $T/trace_$name -o run -- python3 bench.py --no-cpu-baseline --kernel-reps 5 $args > $T/bench_$name.json 2> $T/bench_$name.err || { tail $T/bench_$name.err; exit 1; }
   python3 tools/trace_summary.py $T/trace_$name > $T/trace_$name.txt
