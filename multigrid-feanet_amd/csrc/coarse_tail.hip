@@ -90,7 +90,9 @@ __device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element off
 constexpr int kTailDownRows = 2;  // coarse rows per wave going down: Hc - 2 <= 31 over 16 waves
 constexpr int kTailUpRows = 4;    // fine rows per wave going up / at the coarsest level: H - 2 <= 63
 
-template <typename T, bool MULTI>
+// HT != 0: the grid is HT x HT with NLEV levels, known at compile time (every BASELINE configuration
+// ends in the 65^2 .. 3^2 tail), so level sizes, offsets and rows per wave fold into immediates.
+template <typename T, bool MULTI, int HT = 0>
 struct TailFast {
   const TailArgs<T>& a;
   T* es;               // per-level corrections (up-sweep outputs), level regions like fs
@@ -103,6 +105,9 @@ struct TailFast {
   T* vg;               // row 0 of this sample's v_t
   int ld, wv, lane;
   T kr[9], rr[9], pr[9], om0;
+
+  __device__ __forceinline__ int Hk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Ht, k); }
+  __device__ __forceinline__ int Nk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Wt, k); }
 
   __device__ __forceinline__ T omega(int p) const {
     if constexpr (MULTI) return ktb[p * kTS + 9];
@@ -171,7 +176,7 @@ struct TailFast {
   template <bool GLOBAL, int PER>
   __device__ __forceinline__ void down_rows(int k, int o, int I0, int I1) const {
     constexpr int R = 2 * PER + 3;
-    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    const int H = Hk(k), N = Nk(k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
     T* f = fs + o;
     const uint8_t* pk = pl + o;
     T* fc = fs + o + H * N;
@@ -221,7 +226,7 @@ struct TailFast {
   template <bool GLOBAL>
   __device__ __forceinline__ void down(int k, int o) const {
     constexpr int kWaves = kTailThreads / 64;
-    const int Hc = (tail_n(a.Ht, k) + 1) / 2;
+    const int Hc = (Hk(k) + 1) / 2;
     const int per = (Hc - 2 + kWaves - 1) / kWaves;  // <= kTailDownRows
     const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
     if (I0 >= I1) return;  // wave-uniform
@@ -233,7 +238,7 @@ struct TailFast {
   template <int PER>
   __device__ __forceinline__ void coarsest_rows(int k, int o, int y0, int y1) const {
     constexpr int R = PER + 2;
-    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k);
+    const int H = Hk(k), N = Nk(k);
     const T* f = fs + o;
     const uint8_t* pk = pl + o;
     const int yb = y0 - 1;
@@ -268,7 +273,7 @@ struct TailFast {
   __device__ __forceinline__ void up_rows(int k, int o, int oc, int y0, int y1) const {
     constexpr int R = PER + 2;                // x rows y0-1 .. y0+R-2
     constexpr int C = (PAR + R) / 2 + 1;      // coarse rows Ib .. Ib+C-1 that they touch
-    const int H = tail_n(a.Ht, k), N = tail_n(a.Wt, k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    const int H = Hk(k), N = Nk(k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
     const T* f = fs + o;
     const T* e = es + oc;
     const uint8_t* pk = pl + o;
@@ -343,7 +348,7 @@ struct TailFast {
   }
   __device__ __forceinline__ void up(int k, int o, int oc) const {
     constexpr int kWaves = kTailThreads / 64;
-    const int H = tail_n(a.Ht, k);
+    const int H = Hk(k);
     const int per = (H - 2 + kWaves - 1) / kWaves;
     const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
     if (y0 >= y1) return;
@@ -352,7 +357,7 @@ struct TailFast {
   }
   __device__ __forceinline__ void coarsest(int k, int o) const {
     constexpr int kWaves = kTailThreads / 64;
-    const int H = tail_n(a.Ht, k);
+    const int H = Hk(k);
     const int per = (H - 2 + kWaves - 1) / kWaves;
     const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
     if (y0 >= y1) return;
@@ -365,16 +370,16 @@ struct TailFast {
   }
 };
 
-template <typename T, bool MULTI>
+template <typename T, bool MULTI, int HT = 0, int NLEV = 0>
 __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, const T* ktb, const T* rtb,
                                           const T* ptb, const uint8_t* pl, int wv, int lane
 #ifdef FEA_TAIL_TRACE
                                           , int& nph
 #endif
 ) {
-  const int nlev = a.nlev, Ht = a.Ht, Wt = a.Wt;
+  const int nlev = NLEV ? NLEV : a.nlev;
   const long long s0 = (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1) + a.ld_t;
-  TailFast<T, MULTI> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
+  TailFast<T, MULTI, HT> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
   if constexpr (!MULTI) {  // single-pattern tables in registers (uniform loads)
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
@@ -385,22 +390,35 @@ __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, co
     t.om0 = a.omd[0];
   }
   // ------------------------------------------------------------------ down
+  // (NLEV != 0: the level loops unroll, so k, the level sizes and offsets are constants in every phase)
   int o = 0;
-  for (int k = 0; k + 1 < nlev; ++k) {
+  auto down = [&](int k) {
     if (k == 0) t.template down<true>(k, o);
     else t.template down<false>(k, o);
-    o += tail_n(Ht, k) * tail_n(Wt, k);
+    o += t.Hk(k) * t.Nk(k);
     FEA_TAIL_SYNC();
+  };
+  auto up = [&](int k) {
+    const int oc = o;
+    o -= t.Hk(k) * t.Nk(k);
+    t.up(k, o, oc);
+    if (k > 0) FEA_TAIL_SYNC();
+  };
+  if constexpr (NLEV != 0) {
+#pragma unroll
+    for (int k = 0; k + 1 < NLEV; ++k) down(k);
+  } else {
+    for (int k = 0; k + 1 < nlev; ++k) down(k);
   }
   // ------------------------------------------------------------------ coarsest: 2 sweeps
   t.coarsest(nlev - 1, o);
   if (nlev > 1) FEA_TAIL_SYNC();
   // ------------------------------------------------------------------ up
-  for (int k = nlev - 2; k >= 0; --k) {
-    const int oc = o;
-    o -= tail_n(Ht, k) * tail_n(Wt, k);
-    t.up(k, o, oc);
-    if (k > 0) FEA_TAIL_SYNC();
+  if constexpr (NLEV != 0) {
+#pragma unroll
+    for (int k = NLEV - 2; k >= 0; --k) up(k);
+  } else {
+    for (int k = nlev - 2; k >= 0; --k) up(k);
   }
 }
 
@@ -464,11 +482,18 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     // the first down phase reads f_t from HBM itself and stages it for the up phase; single pattern:
     // the tables come from uniform loads, so nothing has to land before it
     if (MULTI || nlev == 1) FEA_TAIL_SYNC();
-    tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+    if (a.Ht == 65 && a.Wt == 65 && nlev == 6)  // the tail of every BASELINE configuration
+      tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
 #ifdef FEA_TAIL_TRACE
-                        , nph
+                                 , nph
 #endif
-    );
+      );
+    else
+      tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+#ifdef FEA_TAIL_TRACE
+                          , nph
+#endif
+      );
     return;
   }
   FEA_TAIL_SYNC();
