@@ -358,6 +358,10 @@ class MultigridSolver:
         times the top level's nodes."""
         esz = 4 if self.dtype == torch.float32 else 8
         multi = self.ntab > 1
+        if up and os.environ.get("FEANET_MID_UP_TILE"):  # A/B knob: "RxC" rows x columns of the up tiles
+            TR, TC = (int(x) for x in os.environ["FEANET_MID_UP_TILE"].lower().split("x"))
+            if _lib.mid_lds_bytes(up, k, TR, TC, esz, multi) > 0:
+                return (TR, TC)
         tl = self.levels[a if up else a + k]
         top = self.levels[a]
         best = None
@@ -376,8 +380,9 @@ class MultigridSolver:
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
+        cap = int(os.environ.get("FEANET_MID_UP_NODES", self.MID_NODES)) if up else self.MID_NODES
         el = sorted(l for l in levels
-                    if self.B * self.levels[l].H * self.levels[l].W <= self.MID_NODES and l + 1 < self.L)
+                    if self.B * self.levels[l].H * self.levels[l].W <= cap and l + 1 < self.L)
         groups = []
         hi = len(el)
         while hi >= 2:
@@ -436,13 +441,15 @@ class MultigridSolver:
             a, k, T = st[1], st[2], st[3]
             fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + k + 1)])
             pids = _lib.PtrArray([pid(j) for j in range(a, a + k + 1)]) if nt > 1 else None
-            return ("mg_mid_down", (fs, pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt, rt, nr, self.w[0], T, T))
+            TR, TC = T if isinstance(T, tuple) else (T, T)
+            return ("mg_mid_down", (fs, pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt, rt, nr, self.w[0], TR, TC))
         if kind == "mid_up":
             a, k, csrc, dst, T = st[1:6]
             fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + k)])
             pids = _lib.PtrArray([pid(j) for j in range(a, a + k + 1)]) if nt > 1 else None
+            TR, TC = T if isinstance(T, tuple) else (T, T)
             return ("mg_mid_up", (fs, ptr(a + k, csrc), ptr(a, dst), pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt,
-                                  pt, npt, self.w[1], T, T))
+                                  pt, npt, self.w[1], TR, TC))
         if kind == "coarse_tail":
             t = l
             return ("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
