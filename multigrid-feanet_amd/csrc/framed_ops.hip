@@ -1660,6 +1660,10 @@ static int num_cus() {
 // with at least target_waves() waves in flight.  e.g. 4097^2 fp64: 504 workgroups of 74 rows
 // (2 per CU) instead of 576 of 64 (2.25 per CU: a quarter of the CUs run 3).  FEANET_BALANCE=0
 // restores the power-of-two choice (A/B).  Results are bitwise independent of the task height.
+static int rb_occ() {
+  const char* e = getenv("FEANET_RB_OCC");
+  return e ? atoi(e) : 0;
+}
 static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
   const char* e = getenv("FEANET_BALANCE");
   if ((e && atoi(e) == 0) || rows_c < 2) return rb_pow2;
@@ -1670,7 +1674,9 @@ static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
   for (int rbc = 1; rbc <= rows_c && 2 * rbc <= 4 * rb_pow2; ++rbc) {
     const long long ntr = div_up(rows_c, rbc), wgs = (long long)B * div_up(ntr * nstrips, kWaves);  // linear order
     if (wgs < min_wg) break;  // larger tasks only lower the count further
-    const long long cost = div_up(wgs, ncu) * (2 * rbc + halo);
+    // FEANET_RB_OCC = k > 0: cost by rounds of k resident workgroups per CU (A/B knob)
+    const long long occ = rb_occ();
+    const long long cost = (occ > 0 ? div_up(wgs, ncu * occ) * occ : div_up(wgs, ncu)) * (2 * rbc + halo);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
       best = 2 * rbc;
