@@ -458,6 +458,13 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
 constexpr int kRRAhead = FEA_RR_AHEAD;
 static_assert(kRRAhead >= 1 && kRRAhead <= 4, "residual-restriction ring of 1..4 iterations");
 
+#ifdef FEA_RR_TRACE
+__device__ long long g_rr_trace[2 * 8192];
+extern "C" int fea_rr_trace_read(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rr_trace), sizeof(long long) * 2 * 8192, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 template <typename T, bool MULTI, bool ZERO, bool NT>
 __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   using F = Frame<T>;
@@ -471,6 +478,16 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   }
   const TaskId id = decode_task(g.nstrips, g.ntr);
   if (!id.valid) return;
+#ifdef FEA_RR_TRACE  // lab builds only (tools/lab/rr_trace.py): per-wave start / end, s_memrealtime (100 MHz)
+  const int trace_w = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && trace_w < 8192) g_rr_trace[trace_w] = (long long)__builtin_amdgcn_s_memrealtime();
+  struct TraceEnd {
+    int w;
+    __device__ ~TraceEnd() {
+      if ((threadIdx.x & 63) == 0 && w < 8192) g_rr_trace[8192 + w] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+  } trace_end{trace_w};
+#endif
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
   const int c0 = 1 + id.s * F::SW;
