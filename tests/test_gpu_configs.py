@@ -5,7 +5,7 @@ against the single-GPU path, at the configuration's own size.
   C4  8193^2 Poisson fp64 over 8 ranks (slabs, 4 x 2 blocks)   -> bitwise the single-GPU V-cycle,
                                                                    which is checked against the oracle
   C5  256 x 1025^2 fp32 batch                                   -> bitwise per-sample independence,
-                                                                   oracle fp32 residuals of 3 samples
+                                                                   oracle fp32 first cycle of 3 samples
 """
 import os
 
@@ -154,12 +154,19 @@ def test_c5_batch256_1025_fp32():
         s1.load()
         s1.vcycle(3)
         assert torch.equal(s1.solution()[0], ub[b]), b
-    # the oracle's fp32 MultiGrid.Step on the same samples: two fp32 implementations' iterates drift
-    # apart by cond(K) eps32, so the residual norms are compared (as in test_gpu_mg's fp32 cycles)
+    # the oracle's fp32 MultiGrid.Step on three of the samples, first cycle (as test_gpu_mg's fp32
+    # cycles: later fp32 iterates of two implementations drift apart by cond(K) eps32, and with these
+    # smooth sources the residual after 3 cycles is already at that rounding floor, so it is not compared);
+    # the batch-256 run is bitwise these samples' own runs (above)
+    idx = [0, 97, 255]
+    s3 = MultigridSolver(n, dtype=torch.float32, batch=3)
+    s3.set_rhs(f=f[idx])
+    s3.load()
+    s3.vcycle()
     mg = orc.OracleMultigrid(n, "poisson", np.float32)
-    fb = f[[0, 97, 255], 0].cpu().numpy()
-    v = np.zeros_like(fb)
-    for _ in range(3):
-        v = mg.step(v, fb)
-    np.testing.assert_allclose(r3[[0, 97, 255]].cpu().numpy(), mg.residual_norm(v, fb), rtol=2e-3,
-                               atol=1e-6 * float(r0.max()))
+    fb = f[idx, 0].cpu().numpy()
+    v = mg.step(np.zeros_like(fb), fb)
+    got = s3.solution().cpu().numpy()[:, 0]
+    for i in range(3):
+        err = np.abs(got[i] - v[i]).max() / np.abs(v[i]).max()
+        assert err < 2e-5, (idx[i], err)
