@@ -883,6 +883,180 @@ __global__ __launch_bounds__(256) void k_mg_sweep_restrict(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel B0: zero-guess residual + restriction on OVERLAPPED strips (levels >= 1 going down, v not kept):
+//   v = omd f (interior, 0 on the boundary),   f_c = w0 R(f - K v)
+// k_mg_resid_restrict<ZERO> with v_out = NULL, restated: v is local to its node, so a wave forms it on
+// all 64*VEC columns it loads and takes the window neighbours by DPP — no halo loads, K applied at VEC
+// instead of VEC+1 columns per lane and v formed at VEC instead of VEC+3 (the residual of column
+// cl+VEC comes from the next lane).  The per-node expressions and the restriction's 9-term order are
+// those of k_mg_resid_restrict, so f_c is bitwise the same (tests/test_gpu_mg.py::test_mg_transfer).
+// ---------------------------------------------------------------------------
+template <typename T, bool MULTI, bool NT>
+__global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
+  using F = Frame<T>;
+  using O = Ovl<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column
+  const int cs = c0 - V;           // first loaded column
+  const int cl = cs + V * lane;
+  const int I0 = 1 + id.t * (g.rb / 2);
+  const int I1 = min(I0 + g.rb / 2, Hc - 1);
+  T ks[9], rs[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      rs[d] = g.rtab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w0 = g.w;
+  bool cin[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  const bool own = lane >= 1 && lane <= O::OWN;
+  const int J0 = (cl + 1) / 2;
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const T* __restrict__ fb = g.f + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
+  const int ld = g.ld;
+  const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the grid re-read the last needed line
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+
+  struct In {
+    T f[V];
+    int p[V];
+  };
+  struct Wn {  // v window (L, own.., R), f own, pattern window
+    Row<T, V> v;
+    T f[V];
+    PRow<V> p;
+  };
+  auto load = [&](int y) {
+    In r;
+    const long long o = rowo(y);
+    vload<T, V>(fb + o, r.f);
+    if constexpr (MULTI) pload<V>(pb + o, r.p);
+    return r;
+  };
+  auto mk = [&](const In& r, int y) {
+    Wn w;
+    const bool rin = y >= 1 && y <= H - 2;
+    T x[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T omk = MULTI ? tab[r.p[k] * kTabStride + 9] : om;
+      x[k] = (rin && cin[k]) ? omk * r.f[k] : T(0);
+      w.f[k] = r.f[k];
+    }
+    w.v = own_row<T, V>(x);
+    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    return w;
+  };
+  auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) r[k] = b.f[k] - kapply<T, V, MULTI>(a.v, b.v, c.v, a.p, b.p, c.p, k, ks, tab);
+    r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+  };
+
+  const int y0 = 2 * I0 - 1;
+  Wn X0 = mk(load(y0 - 1), y0 - 1);
+  Wn X1 = mk(load(y0), y0);
+  Wn X2 = mk(load(y0 + 1), y0 + 1);
+  constexpr int D = kRRAhead;
+  In ring[D][2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ring[d][0] = load(2 * I0 + 1 + 2 * d);
+    ring[d][1] = load(2 * I0 + 2 + 2 * d);
+  }
+  T Ra[V + 1], Rb[V + 1], Rc[V + 1];
+  PRow<V> Pa = X1.p, Pb, Pc;
+  resid(X0, X1, X2, Ra);
+  auto iter = [&](int I, auto slot) {
+    constexpr int S = decltype(slot)::value;
+    X0 = X1;  // fine row 2I
+    X1 = X2;
+    X2 = mk(ring[S][0], 2 * I + 1);
+    ring[S][0] = load(2 * I + 1 + 2 * D);
+    resid(X0, X1, X2, Rb);
+    Pb = X1.p;
+    X0 = X1;  // fine row 2I+1
+    X1 = X2;
+    X2 = mk(ring[S][1], 2 * I + 2);
+    ring[S][1] = load(2 * I + 2 + 2 * D);
+    resid(X0, X1, X2, Rc);
+    Pc = X1.p;
+    T o[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      T acc;
+      if constexpr (!MULTI) {
+        acc = rs[0] * Ra[2 * q];
+        acc += rs[1] * Ra[2 * q + 1];
+        acc += rs[2] * Ra[2 * q + 2];
+        acc += rs[3] * Rb[2 * q];
+        acc += rs[4] * Rb[2 * q + 1];
+        acc += rs[5] * Rb[2 * q + 2];
+        acc += rs[6] * Rc[2 * q];
+        acc += rs[7] * Rc[2 * q + 1];
+        acc += rs[8] * Rc[2 * q + 2];
+      } else {
+        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
+        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
+        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
+        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
+        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
+        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
+        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
+        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
+        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+      }
+      o[q] = w0 * acc;
+    }
+    if (own) {
+      T* cp = cb + (long long)(I + 1) * g.ldc;
+      if (J0 + Q - 1 <= Wc - 2) {
+        vstore<T, Q, kCoarseNT && NT>(cp, o);
+      } else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (J0 + q <= Wc - 2) cp[q] = o[q];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
+    Pa = Pc;
+  };
+  int I = I0;
+  for (; I + D - 1 < I1; I += D) {
+    iter(I, std::integral_constant<int, 0>{});
+    if constexpr (D > 1) iter(I + 1, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 2) iter(I + 2, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 3) iter(I + 3, std::integral_constant<int, 3 % D>{});
+  }
+  if constexpr (D > 1)
+    if (I < I1) iter(I, std::integral_constant<int, 0>{});
+  if constexpr (D > 2)
+    if (I + 1 < I1) iter(I + 1, std::integral_constant<int, 1 % D>{});
+  if constexpr (D > 3)
+    if (I + 2 < I1) iter(I + 2, std::integral_constant<int, 2 % D>{});
+}
+
+// ---------------------------------------------------------------------------
 // Kernel C: fused prolongation + correction (+ post-sweep):
 //   v = u + w1 * P(ec)   (P kernel of the coarse node);   out = SWEEP ? J(v, f) : v
 // ZU (with SWEEP): the level's iterate is its zero-guess pre-sweep u = omd*f (interior, 0 on the
@@ -1711,6 +1885,13 @@ static long long nt_bytes() {
   return e ? atoll(e) : (64ll << 20);
 }
 
+// zero-guess residual-restriction without a kept v on overlapped strips (k_mg_zero_restrict; bitwise the
+// per-lane-halo kernel, which FEANET_ZR_OVL=0 selects for A/B)
+static bool zero_ovl() {
+  const char* e = getenv("FEANET_ZR_OVL");
+  return !(e && atoi(e) == 0);
+}
+
 // rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
 static int join_max_rb() {
   const char* e = getenv("FEANET_JOIN_RB");
@@ -1874,10 +2055,19 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
     g.bsc = bsc;                                                                                             \
     g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
-    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
+    if (!u && !v_out && zero_ovl()) { /* zero guess, v not kept: overlapped strips (k_mg_zero_restrict) */  \
+      g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                  \
+      g.rb = pick_rb(B, g.nstrips, H - 2);                                                                   \
+      g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                    \
+      const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                    \
+      if (multi) FEA_NT_LAUNCH(k_mg_zero_restrict, T COMMA true)                                             \
+      else FEA_NT_LAUNCH(k_mg_zero_restrict, T COMMA false)                                                  \
+      FEA_LAUNCH_CHECK();                                                                                    \
+    }                                                                                                        \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     if (!u) {                                                                                                \
       if (multi) FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA true COMMA true)                                 \
       else FEA_NT_LAUNCH(k_mg_resid_restrict, T COMMA false COMMA true)                                      \
