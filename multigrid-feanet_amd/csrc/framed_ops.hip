@@ -1337,6 +1337,201 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Kernel C0: k_mg_prolong<SWEEP, ZU> (levels >= 1 going up) on OVERLAPPED strips:
+//   x = omd f + w1 P(ec)  (interior),   out = J(x, f)
+// x of a node needs only its own f and the coarse nodes left of and under it, so a wave forms x on the
+// columns it loads (the coarse left neighbour by DPP) and takes the sweep's window neighbours by DPP: no
+// halo loads, the correction at VEC instead of VEC+2 columns per lane and omd f at VEC instead of VEC+3.
+// Lanes 1..OWN store.  Same per-node expressions (crow_term, correction order, sweep) as k_mg_prolong,
+// so the output is bitwise the same.
+// ---------------------------------------------------------------------------
+template <typename T, bool MULTI, bool NT>
+__global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
+  using F = Frame<T>;
+  using O = Ovl<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, ptb, g.ptab, g.nptab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int H = g.H, Hc = g.Hc, W = g.W;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column
+  const int cs = c0 - V;           // first loaded column
+  const int cl = cs + V * lane;    // odd
+  const int r0 = 1 + id.t * g.rb;  // odd
+  const int r1 = min(r0 + g.rb, H - 1);
+  T ks[9], ps[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      ps[d] = g.ptab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w1 = g.w;
+  const int ld = g.ld, ldc = g.ldc;
+  bool cin[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  const bool own = lane >= 1 && lane <= O::OWN;
+  const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the grid re-read the last needed line
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ ob = g.out + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  const int jc = (cs + 1) / 2;  // coarse column of lane 0's first own coarse node
+  const long long pcoff = F::OFF + jc;
+  const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + pcoff;
+  const uint8_t* __restrict__ pcb = MULTI ? g.pidc + pcoff : nullptr;
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+  auto crowo = [&](int a) -> long long { return (long long)(min(a, Hc) + 1) * ldc + Q * ll; };
+
+  struct In {
+    T f[V];
+    int p[V];
+  };
+  struct RC {
+    T x[Q];
+    int p[Q];
+  };
+  struct XR {  // window row of the corrected iterate x, its pattern window, f's own columns
+    Row<T, V> x;
+    PRow<V> p;
+    T f[V];
+  };
+  auto ld_f = [&](int y) {
+    In r;
+    const long long o = rowo(y);
+    vload<T, V>(fb + o, r.f);
+    if constexpr (MULTI) pload<V>(pb + o, r.p);
+    return r;
+  };
+  auto ld_c = [&](int a) {
+    RC r;
+    const long long o = crowo(a);
+    vload<T, Q>(eb + o, r.x);
+    if constexpr (MULTI) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) r.p[q] = pcb[o + q];
+    }
+    return r;
+  };
+  auto fin_c = [&](const RC& r) {  // e[0] = the left lane's last coarse node, e[1..Q] own (e[Q+1] unused)
+    CRow<T, V> c{};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c.e[q + 1] = r.x[q];
+    c.e[0] = shr1(r.x[Q - 1], T(0));
+    if constexpr (MULTI) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * kTabStride;
+      c.o[0] = shr1(r.p[Q - 1], 0) * kTabStride;
+    }
+    return c;
+  };
+  // omd f of row y on the lane's own columns, then the correction of an even (ky = 1) or odd row
+  auto zero_iterate = [&](const In& r, int y, T (&x)[V]) {
+    const bool rin = y >= 1 && y <= H - 2;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T omk = MULTI ? tab[r.p[k] * kTabStride + 9] : om;
+      x[k] = (rin && cin[k]) ? omk * r.f[k] : T(0);
+    }
+  };
+  auto finish_x = [&](const In& r, const T (&x)[V]) {
+    XR w;
+    w.x = own_row<T, V>(x);
+    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+#pragma unroll
+    for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
+    return w;
+  };
+  auto row_even = [&](const In& r, int y, const CRow<T, V>& ca) {
+    T x[V];
+    zero_iterate(r, y, x);
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] += w1 * crow_term<T, V, MULTI>(ca, k + 1, 1, ps, ptb);
+    return finish_x(r, x);
+  };
+  auto row_odd = [&](const In& r, int y, const CRow<T, V>& ca, const CRow<T, V>& cb) {
+    T x[V];
+    zero_iterate(r, y, x);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T t = crow_term<T, V, MULTI>(ca, k + 1, 2, ps, ptb) + crow_term<T, V, MULTI>(cb, k + 1, 0, ps, ptb);
+      x[k] += w1 * t;
+    }
+    return finish_x(r, x);
+  };
+  auto emit = [&](int y, const XR& a, const XR& b, const XR& c) {
+    T o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T acc = kapply<T, V, MULTI>(a.x, b.x, c.x, a.p, b.p, c.p, k, ks, tab);
+      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      o[k] = omk * (b.f[k] - acc) + b.x.a[k + 1];
+    }
+    if (own) store_masked<T, V, NT>(ob + rowo(y), o, cl, W);
+  };
+
+  // window rows r0-1 (even, coarse a0) and r0 (odd, coarse a0, a0+1)
+  const int a0 = (r0 - 1) / 2;
+  const CRow<T, V> C0 = fin_c(ld_c(a0));
+  CRow<T, V> C1 = fin_c(ld_c(a0 + 1));
+  XR Xp = row_even(ld_f(r0 - 1), r0 - 1, C0);
+  XR Xc = row_odd(ld_f(r0), r0, C0, C1);
+  // iteration y (odd) emits rows y and y+1 from fine rows y+1, y+2 and coarse row (y+3)/2, whose loads
+  // are in flight kProlongAhead iterations ahead (ring slots consumed in place, refilled at once)
+  constexpr int D = kProlongAhead;
+  struct Slot {
+    In u1, u2;
+    RC c;
+  };
+  Slot ring[D];
+  auto fill = [&](Slot& sl, int y) {
+    sl.u1 = ld_f(y + 1);
+    sl.u2 = ld_f(y + 2);
+    sl.c = ld_c((y + 3) / 2);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) fill(ring[d], r0 + 2 * d);
+  auto iter = [&](int y, auto slot) {
+    Slot& sl = ring[decltype(slot)::value];
+    const XR Xn = row_even(sl.u1, y + 1, C1);  // row y+1 (even, coarse (y+1)/2 = C1)
+    emit(y, Xp, Xc, Xn);
+    if (y + 1 < r1) {  // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
+      const CRow<T, V> C2 = fin_c(sl.c);
+      const XR Xnn = row_odd(sl.u2, y + 2, C1, C2);
+      emit(y + 1, Xc, Xn, Xnn);
+      Xp = Xn;
+      Xc = Xnn;
+      C1 = C2;
+    }
+    fill(sl, y + 2 * D);
+  };
+  int y = r0;
+  for (; y + 2 * (D - 1) < r1; y += 2 * D) {
+    iter(y, std::integral_constant<int, 0>{});
+    if constexpr (D > 1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 2) iter(y + 4, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 3) iter(y + 6, std::integral_constant<int, 3 % D>{});
+  }
+  if constexpr (D > 1)
+    if (y < r1) iter(y, std::integral_constant<int, 0>{});
+  if constexpr (D > 2)
+    if (y + 2 < r1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+  if constexpr (D > 3)
+    if (y + 4 < r1) iter(y + 4, std::integral_constant<int, 2 % D>{});
+}
+
+// ---------------------------------------------------------------------------
 // Kernel F: cycle join — the post-smooth of V-cycle k and the pre-smooth + residual + restriction
 // of V-cycle k+1 on one level in ONE pass (temporal blocking across the cycle boundary):
 //   x = u + w1 P(ec)        (FEANet/multigrid.py:177-180, prolongation + correction)
@@ -1892,6 +2087,18 @@ static bool zero_ovl() {
   return !(e && atoi(e) == 0);
 }
 
+// prolongation + sweep of a recomputed zero-guess iterate on overlapped strips (k_mg_prolong_zu_ovl; bitwise
+// k_mg_prolong<ZU>) on levels of at most FEANET_PZ_OVL_BYTES (default 16 MiB): there the shorter per-wave
+// chain pays (1025^2 fp64: 6.1 -> 5.5 us); on larger levels the fine output dominates and the owned strips
+// (122 of 128 columns) split 128-byte lines between two waves' stores (2049^2: 14.6 -> 15.0 us, same-lease
+// A/B, profiles/r02_ab/prolong_ovl).  FEANET_PZ_OVL=0 turns it off.
+static bool zu_ovl(long long level_bytes) {
+  const char* e = getenv("FEANET_PZ_OVL");
+  if (e && atoi(e) == 0) return false;
+  const char* b = getenv("FEANET_PZ_OVL_BYTES");
+  return level_bytes <= (b ? atoll(b) : (16ll << 20));
+}
+
 // rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
 static int join_max_rb() {
   const char* e = getenv("FEANET_JOIN_RB");
@@ -2131,8 +2338,17 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.u = u; g.ec = ec; g.f = f; g.out = out; g.pid = pid; g.pidc = pidc; g.ktab = ktab; g.omd = omd;         \
     g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2;          \
     g.ldc = ldc; g.bsc = bsc;                                                                                \
-    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (sweep && !u && zu_ovl((long long)B * bs * (long long)sizeof(T))) { /* small levels: overlapped strips */  \
+      g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                  \
+      g.rb = pick_rb(B, g.nstrips, H - 2);                                                                   \
+      g.ntr = div_up(H - 2, g.rb);                                                                           \
+      const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                    \
+      if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true)                                            \
+      else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false)                                                 \
+      FEA_LAUNCH_CHECK();                                                                                    \
+    }                                                                                                        \
+    const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     if (sweep && !u) {                                                                                       \
       if (multi) FEA_NT_LAUNCH_ZU(k_mg_prolong, T COMMA true COMMA true)                                     \
       else FEA_NT_LAUNCH_ZU(k_mg_prolong, T COMMA false COMMA true)                                          \
