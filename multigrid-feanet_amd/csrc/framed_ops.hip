@@ -681,6 +681,15 @@ struct Ovl {
   static constexpr int S = ((63 * V - 3) / V) * V;  // owned fine columns per strip (mult. of V)
   static constexpr int OWN = S / V;                 // owning lanes: 1 .. OWN
 };
+// owned strips of whole 128-byte lines (lanes 1..56 own, 57..63 only feed their neighbours): for kernels
+// whose fine-level STORES dominate, so no line is written by two waves
+template <typename T>
+struct OvlA {
+  static constexpr int V = Frame<T>::VEC;
+  static constexpr int S = 56 * V;
+  static constexpr int OWN = S / V;
+  static_assert(S % Frame<T>::A == 0, "line-aligned owned strips");
+};
 
 template <typename T, int V>
 __device__ __forceinline__ Row<T, V> own_row(const T (&x)[V]) {  // window L, own.., R from own values
@@ -1345,10 +1354,10 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 // Lanes 1..OWN store.  Same per-node expressions (crow_term, correction order, sweep) as k_mg_prolong,
 // so the output is bitwise the same.
 // ---------------------------------------------------------------------------
-template <typename T, bool MULTI, bool NT>
+template <typename T, bool MULTI, bool ALIGN, bool NT>
 __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
   using F = Frame<T>;
-  using O = Ovl<T>;
+  using O = std::conditional_t<ALIGN, OvlA<T>, Ovl<T>>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
@@ -2092,11 +2101,16 @@ static bool zero_ovl() {
 // chain pays (1025^2 fp64: 6.1 -> 5.5 us); on larger levels the fine output dominates and the owned strips
 // (122 of 128 columns) split 128-byte lines between two waves' stores (2049^2: 14.6 -> 15.0 us, same-lease
 // A/B, profiles/r02_ab/prolong_ovl).  FEANET_PZ_OVL=0 turns it off.
-static bool zu_ovl(long long level_bytes) {
+// Larger levels: FEANET_PZ_BIG = 0 keeps k_mg_prolong<ZU>, 1 the same overlapped strips, 2 line-aligned owned
+// strips (OvlA).  Returns 0 (k_mg_prolong<ZU>), 1 (Ovl) or 2 (OvlA).
+static int zu_ovl(long long level_bytes) {
   const char* e = getenv("FEANET_PZ_OVL");
-  if (e && atoi(e) == 0) return false;
+  if (e && atoi(e) == 0) return 0;
   const char* b = getenv("FEANET_PZ_OVL_BYTES");
-  return level_bytes <= (b ? atoll(b) : (16ll << 20));
+  if (level_bytes <= (b ? atoll(b) : (16ll << 20))) return 1;
+  const char* big = getenv("FEANET_PZ_BIG");
+  const int m = big ? atoi(big) : 0;
+  return (m >= 0 && m <= 2) ? m : 0;
 }
 
 // rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
@@ -2339,13 +2353,19 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2;          \
     g.ldc = ldc; g.bsc = bsc;                                                                                \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    if (sweep && !u && zu_ovl((long long)B * bs * (long long)sizeof(T))) { /* small levels: overlapped strips */  \
-      g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                  \
+    const int zm = (sweep && !u) ? zu_ovl((long long)B * bs * (long long)sizeof(T)) : 0;                    \
+    if (zm) { /* overlapped strips */                                                                        \
+      g.nstrips = div_up(W - 2, zm == 2 ? OvlA<T>::S : Ovl<T>::S);                                           \
       g.rb = pick_rb(B, g.nstrips, H - 2);                                                                   \
       g.ntr = div_up(H - 2, g.rb);                                                                           \
       const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                    \
-      if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true)                                            \
-      else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false)                                                 \
+      if (zm == 2) {                                                                                         \
+        if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true COMMA true)                               \
+        else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false COMMA true)                                    \
+      } else {                                                                                               \
+        if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true COMMA false)                              \
+        else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false COMMA false)                                   \
+      }                                                                                                      \
       FEA_LAUNCH_CHECK();                                                                                    \
     }                                                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \

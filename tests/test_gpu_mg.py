@@ -847,3 +847,53 @@ def test_pipelined_state_semantics():
         out.append(rec)
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+ZVARIANT_ENV = ("FEANET_ZR_OVL", "FEANET_PZ_OVL", "FEANET_PZ_OVL_BYTES", "FEANET_PZ_BIG")
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n,m,B", [("poisson", 4, None, 1), ("poisson", 16, None, 2), ("poisson", 128, None, 1),
+                                           ("poisson", 1024, None, 1), ("poisson", 256, 64, 2),
+                                           ("interface", 32, None, 3), ("interface", 256, None, 1)])
+def test_zero_guess_kernel_variants_bitwise(T, problem, n, m, B, monkeypatch):
+    """The zero-guess level kernels have several launch forms chosen per level size: the residual-restriction
+    with per-lane halos (FEANET_ZR_OVL=0) or on overlapped strips (k_mg_zero_restrict); the prolongation +
+    sweep of the recomputed iterate omd f as k_mg_prolong<ZU> (FEANET_PZ_OVL=0), on overlapped strips, or on
+    line-aligned owned strips (every level counted as large, FEANET_PZ_BIG=2).  All are bitwise the same,
+    including rows != columns and per-pattern learned R/P."""
+    from feanet_amd import _lib
+    rng = np.random.default_rng(13 * n + B)
+    fr = Frame(n, B, T, problem, m=m)
+    co = Frame(n // 2, B, T, problem, m=None if m is None else m // 2)
+    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned=problem == "interface")
+    nt = ktab.shape[0]
+    u, f = rand_state(rng, B, (fr.H, fr.W), T)
+    fr.put("f", f)
+    e = rng.standard_normal((B, co.H, co.W)).astype(npdt(T))
+    e[:, 0, :] = e[:, -1, :] = e[:, :, 0] = e[:, :, -1] = 0
+
+    def run(env, what):
+        for k in ZVARIANT_ENV:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        if what == "rr":
+            co.put("f", e * 0 + 3.0)
+            _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), None, co.L.f.data_ptr(), fr.pid(),
+                      kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *fr.args(), co.L.ld, co.L.bs, None)
+            return co.get("f")
+        co.put("a", e)
+        fr.put("b", u * 0 + 7.0)
+        _lib.call("mg_prolong_sweep", T, None, co.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), fr.pid(),
+                  co.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, 0.75, *fr.args(), co.L.ld,
+                  co.L.bs, None)
+        return fr.get("b")
+
+    rr = [run(env, "rr") for env in ({"FEANET_ZR_OVL": "0"}, {})]
+    assert np.array_equal(rr[0], rr[1])
+    ps = [run(env, "ps") for env in ({"FEANET_PZ_OVL": "0"}, {}, {"FEANET_PZ_OVL_BYTES": "0", "FEANET_PZ_BIG": "1"},
+                                     {"FEANET_PZ_OVL_BYTES": "0", "FEANET_PZ_BIG": "2"})]
+    for i in (1, 2, 3):
+        assert np.array_equal(ps[0], ps[i]), i
+    assert (ps[0][:, 0, :] == 7).all() and (ps[0][:, :, -1] == 7).all()
