@@ -7,8 +7,12 @@ Reference bugs fixed here: SingleGrid.Relax loops single sweeps inst
 an `n_iter=` argument jacobi_convolution does not accept.  Buffers are allocated on the input's
 device/dtype instead of hard-coded CPU float32.
 
-`MultiGrid.iterate` runs the fused MultigridSolver V-cycle when no autograd graph is needed
-(inference) and the module-level operators otherwise; both compute the reference's schedule.
+`MultiGrid.iterate` always runs the fused MultigridSolver V-cycle forward (the custom op
+torch.ops.feanet.mg_step).  When autograd is recording and an input or the R/P weights need a gradient,
+the call is wrapped in `_FusedIterate`: its backward recomputes the cycle from the module-level HIP
+operators (each with a registered HIP adjoint) and back-propagates through that, so the detached
+iterations of `forward` (the first m-1 of m, multigrid.py:147-150) never pay for the per-op path.
+Both paths compute the reference's schedule.
 """
 import numpy as np
 import torch
@@ -89,6 +93,31 @@ class ProlongationNet(nn.Module):
         return ops.prolong(x_split, self.net.weight[:, 0], 1.0)
 
 
+class _FusedIterate(torch.autograd.Function):
+    """Forward: the fused V-cycle.  Backward: gradients of the same cycle as composed from the module-level
+    operators (`iterate_modules`), recomputed from the saved inputs — the fused forward keeps no per-level
+    intermediates, so the adjoint cycle needs them rebuilt once, only when a gradient is actually asked for."""
+
+    @staticmethod
+    def forward(ctx, x, f, wr, wp, w, mg):
+        ctx.mg = mg
+        ctx.save_for_backward(x, f)
+        return mg._fused(x).step(x, f)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, f = ctx.saved_tensors
+        mg = ctx.mg
+        params = (mg.conv.net.weight, mg.deconv.net.weight, mg.w)
+        with torch.enable_grad():
+            xd = x.detach().requires_grad_(ctx.needs_input_grad[0])
+            fd = f.detach().requires_grad_(ctx.needs_input_grad[1])
+            out = mg.iterate_modules(xd, fd)
+            wanted = [t for t, need in zip((xd, fd) + params, ctx.needs_input_grad[:5]) if need]
+            got = iter(torch.autograd.grad(out, wanted, g, allow_unused=True))
+        return tuple(next(got) if need else None for need in ctx.needs_input_grad[:5]) + (None,)
+
+
 class MultiGrid(nn.Module):
     """V-cycle with learned R/P and ratios w on the two-material problem (multigrid.py:75-185)."""
 
@@ -164,14 +193,17 @@ class MultiGrid(nn.Module):
         return self._solver
 
     def iterate(self, x, f):
-        """One V-cycle (multigrid.py:159-185)."""
+        """One V-cycle (multigrid.py:159-185): the fused solver forward; differentiable through _FusedIterate
+        when autograd records (recomputed module-level cycle in backward)."""
+        params = (self.conv.net.weight, self.deconv.net.weight, self.w)
         needs_grad = torch.is_grad_enabled() and (x.requires_grad or f.requires_grad or any(
-            p.requires_grad for p in (self.conv.net.weight, self.deconv.net.weight, self.w)))
-        if not needs_grad and x.device.type == "cuda":
+            p.requires_grad for p in params))
+        if needs_grad:
+            v = _FusedIterate.apply(x, f, *params, self)
+        else:
             v = self._fused(x).step(x, f)
-            self.grids[0].v, self.grids[0].f = v, f
-            return v
-        return self.iterate_modules(x, f)
+        self.grids[0].v, self.grids[0].f = v, f
+        return v
 
     def iterate_modules(self, x, f):
         """The same V-cycle composed from the module-level HIP operators (autograd-free forward)."""

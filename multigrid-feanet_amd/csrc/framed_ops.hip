@@ -154,10 +154,10 @@ struct RawP {
   int x[V], h[V];
 };
 
-template <typename T, int V>
+template <typename T, int V, bool NTL = false>
 __device__ __forceinline__ RawRow<T, V> raw_row(const T* __restrict__ rp, int lane) {
   RawRow<T, V> r;
-  vload<T, V>(rp + V * lane, r.x);
+  vload<T, V, NTL>(rp + V * lane, r.x);
   // halo: only the two edge lanes load (exec-masked), the other lanes' h is never read
 #pragma unroll
   for (int k = 0; k < V; ++k) r.h[k] = T(0);
@@ -359,6 +359,11 @@ __device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int 
 // ---------------------------------------------------------------------------
 // Kernel A: interior Jacobi sweep  out = J(u, f);  ZERO: u == 0  ->  out = omd * f
 // ---------------------------------------------------------------------------
+// FEA_SWEEP_NTL (lab A/B): nontemporal loads of u and f on levels above the NT threshold
+#ifndef FEA_SWEEP_NTL
+#define FEA_SWEEP_NTL 0
+#endif
+constexpr bool kSweepNTL = FEA_SWEEP_NTL != 0;
 template <typename T, bool MULTI, bool ZERO, bool NT>
 __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   using F = Frame<T>;
@@ -404,11 +409,11 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
       store_masked<T, V, NT>(ob + ro, o, cl, W);
     }
   } else {
-    Row<T, V> w0 = finish(raw_row<T, V>(ub + rowo(r0 - 1), lane));
-    Row<T, V> w1 = finish(raw_row<T, V>(ub + rowo(r0), lane));
-    RawRow<T, V> nx = raw_row<T, V>(ub + rowo(r0 + 1), lane);
+    Row<T, V> w0 = finish(raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0 - 1), lane));
+    Row<T, V> w1 = finish(raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0), lane));
+    RawRow<T, V> nx = raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0 + 1), lane);
     T fx[V];
-    vload<T, V>(fb + rowo(r0) + V * lane, fx);
+    vload<T, V, kSweepNTL && NT>(fb + rowo(r0) + V * lane, fx);
     PRow<V> p0{}, p1{}, p2{};
     RawP<V> px{};
     if constexpr (MULTI) {
@@ -418,9 +423,9 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
     }
     for (int r = r0; r < r1; ++r) {
       // issue next iteration's loads before this row's arithmetic
-      const RawRow<T, V> nn = raw_row<T, V>(ub + rowo(r + 2), lane);
+      const RawRow<T, V> nn = raw_row<T, V, kSweepNTL && NT>(ub + rowo(r + 2), lane);
       T fn[V];
-      vload<T, V>(fb + rowo(r + 1) + V * lane, fn);
+      vload<T, V, kSweepNTL && NT>(fb + rowo(r + 1) + V * lane, fn);
       RawP<V> pn{};
       if constexpr (MULTI) pn = raw_prow<V>(pb + rowo(r + 2), lane);
       const Row<T, V> w2 = finish(nx);
@@ -1574,6 +1579,11 @@ static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of
 #define FEA_JOIN_NTL 1
 #endif
 constexpr bool kJoinNTL = FEA_JOIN_NTL != 0;
+// FEA_JOIN_NTF (lab A/B): nontemporal loads of the right-hand side f too
+#ifndef FEA_JOIN_NTF
+#define FEA_JOIN_NTF 0
+#endif
+constexpr bool kJoinNTF = FEA_JOIN_NTF != 0;
 // FEA_JOIN_ALT: odd row tasks stream bottom-up (see join_task).  FEA_JOIN_SHARED: the rows two tasks
 // share are loaded through the cache instead of nontemporally (with FEA_JOIN_NTL).  Same-lease A/B at
 // 4097^2 fp64 (profiles/r02_ab): ALT=1 join 82.6 us, 348 MB read per launch; ALT=0 84.3 us, 385 MB;
@@ -1695,7 +1705,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
 #pragma unroll
   for (int q = 0; q < kJoinAhead; ++q) {
     load_u(yb + S * q, ub_[q]);
-    vload<T, V>(fb + rowo(yb + S * (q - 1)), fb_[q]);
+    vload<T, V, kJoinNTF && NT>(fb + rowo(yb + S * (q - 1)), fb_[q]);
     if constexpr (MULTI) pload<V>(pb + rowo(yb + S * q), pb_[q]);
   }
   // coarse rows: Ca = the row an even step uses, Cb = the next one in streaming order
@@ -1744,7 +1754,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
       if constexpr (MULTI) p0[k] = bp[k];
     }
     load_u(y + S * kJoinAhead, bu);
-    vload<T, V>(fb + rowo(y + S * (kJoinAhead - 1)), bf);
+    vload<T, V, kJoinNTF && NT>(fb + rowo(y + S * (kJoinAhead - 1)), bf);
     if constexpr (MULTI) pload<V>(pb + rowo(y + S * kJoinAhead), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
     T x[V];

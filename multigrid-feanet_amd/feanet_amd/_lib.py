@@ -86,7 +86,7 @@ def lib():
     if not os.path.exists(LIB):
         raise RuntimeError(f"feanet_amd: {LIB} is missing; run `python -m feanet_amd.build` "
                            "(there is no CPU fallback for the HIP path)")
-    L = ctypes.CDLL(os.environ.get("FEANET_LIB_OVERRIDE", LIB))  # override: A/B tuning builds only
+    L = ctypes.CDLL(LIB)  # (A/B builds of tools/lab replace the module attribute LIB: tools/lab/with_lib.py)
     for name, (args, res) in _EXTRA.items():
         fn = getattr(L, name)
         fn.argtypes = args

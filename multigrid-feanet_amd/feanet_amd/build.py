@@ -31,7 +31,7 @@ def needs_build():
 
 
 def build(force=False, verbose=True, out=None, defines=()):
-    """out / defines: A/B variant libraries for tools/ (loaded with FEANET_LIB_OVERRIDE).
+    """out / defines: A/B variant libraries for tools/ (run a script against one with tools/lab/with_lib.py).
     Each source compiles to its own object in parallel (no device code crosses translation units),
     then one link step."""
     if out is None and not force and not needs_build():

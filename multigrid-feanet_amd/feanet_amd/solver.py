@@ -16,15 +16,28 @@ The launch sequence of one V-cycle is built once (a list of C-ABI calls with fix
 pointers) and replayed as a HIP graph.  Everything stays on the device; the only host syncs
 are the ones a caller asks for (e.g. `.item()` on the residual norm, as the reference drivers do).
 """
+import itertools
 import math
 import os
 import time
+import weakref
 
 import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
 from .schedule import OMDF, group_mid, hjac_schedule, vcycle_schedule
+
+
+_SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
+_HANDLES = itertools.count(1)
+
+
+def solver_by_handle(h):
+    s = _SOLVERS.get(int(h))
+    if s is None:
+        raise RuntimeError(f"feanet: no live MultigridSolver with handle {h}")
+    return s
 
 
 class _Level:
@@ -228,10 +241,15 @@ class MultigridSolver:
         self._sws = None  # solve(): per-cycle partial norm sets of a graph block
         self._bc_version = object()  # identity changes with every set_boundary (third-buffer packing)
         self._c_bc = None
+        # Dirichlet data the finest iterate buffers a/b carry: set_boundary takes effect at the next load(),
+        # and the third buffer c (a materialised end iterate) is packed with the same data as a/b
+        self._ab_bc, self._ab_version = None, self._bc_version
         self._plans = {}
         self._graphs = {}
         self._eager_runs = {}
         self.mass = ms.mass_stencil(size / n)
+        self.handle = next(_HANDLES)  # torch.ops.feanet.mg_step(u, f, handle, cycles)
+        _SOLVERS[self.handle] = self
 
     # ------------------------------------------------------------------ problem data
     @property
@@ -304,9 +322,10 @@ class MultigridSolver:
         self._pack(u0, L0.a, bc=bc)
         self._pack(u0, L0.b, bc=bc)  # both ping-pong buffers carry the boundary values
         self._mid = None
-        if L0.c is not None and self._c_bc is not self._bc_version:
+        self._ab_bc, self._ab_version = bc, self._bc_version
+        if L0.c is not None and self._c_bc is not self._ab_version:
             self._pack(u0, L0.c, bc=bc)  # c only needs the Dirichlet values on its boundary nodes
-            self._c_bc = self._bc_version
+            self._c_bc = self._ab_version
         self._state = "a"
         if self.smoother == "hjac":
             # HRelax forms J(u) - u with the iterate the driver passed, before reset_boundary
@@ -543,13 +562,14 @@ class MultigridSolver:
         return blocks
 
     def _ensure_c(self):
-        """The finest level's third buffer with the Dirichlet values on its boundary nodes (its interior is
-        always written before it is read)."""
+        """The finest level's third buffer with the Dirichlet values of the iterate buffers a/b on its boundary
+        nodes (its interior is always written before it is read; a set_boundary() not yet followed by a load()
+        does not show, as in the unjoined solver)."""
         L0 = self.levels[0]
-        if L0.c is None or self._c_bc is not self._bc_version:
+        if L0.c is None or self._c_bc is not self._ab_version:
             L0.buf("c")
-            self._pack(None, L0.c, bc=getattr(self, "_bc", None))
-            self._c_bc = self._bc_version
+            self._pack(None, L0.c, bc=self._ab_bc)
+            self._c_bc = self._ab_version
 
     def _collapse(self):
         """Leave the pipelined state: the last cycle's end iterate recomputed (PS(0) from the join's
@@ -625,6 +645,11 @@ class MultigridSolver:
         if self._joinable() and not getattr(self, "_hjac_first", False):
             self._vcycles_pipelined(k)
             return
+        self._vcycles_plain(k)
+
+    def _vcycles_plain(self, k):
+        """k unjoined V-cycles (one replay of the whole-cycle plan each) from the materialised iterate."""
+        self._collapse()
         for _ in range(k):
             plan, end = self._plan(self._state)
             if getattr(self, "_hjac_first", False):
@@ -653,12 +678,26 @@ class MultigridSolver:
                 g.replay()
             self._state = end
 
-    def step(self, u, f):
-        """Functional form of MultiGrid.Step / MultiGrid.iterate: one V-cycle from u with rhs f,
-        returns the new fine iterate."""
+    def step(self, u, f, cycles=1):
+        """Functional form of MultiGrid.Step / MultiGrid.iterate: `cycles` V-cycles from u with rhs f,
+        returns the new fine iterate — through the custom op torch.ops.feanet.mg_step (MultiGrid.iterate's
+        fused path takes the same op)."""
+        from . import torch_ops  # noqa: F401  (registers torch.ops.feanet.mg_step)
+        return torch.ops.feanet.mg_step(u, f, self.handle, int(cycles))
+
+    def _step(self, u, f, cycles=1):
+        """Body of feanet::mg_step.  One cycle from a freshly loaded iterate, read at once, runs the unjoined
+        plan (SR(0) + coarse levels + PS(0), 52 B per fine node): the pipelined form would add a cycle join's
+        next pre-smooth and a recomputed post-smooth that nothing reads.  More cycles run joined."""
+        if cycles < 1:
+            raise ValueError("MultigridSolver.step: cycles must be >= 1")
+        self._mid = None  # whatever a previous call left in flight is replaced by u below
         self.set_rhs(f=f)
         self.load(u)
-        self.vcycle()
+        if cycles == 1:
+            self._vcycles_plain(1)
+        else:
+            self.vcycle(cycles)
         return self.solution()
 
     def solve(self, u0=None, f=None, F=None, eps=1e-6, max_cycles=100, bc_value=None):

@@ -17,6 +17,9 @@ FEANet drop-in modules and feanet_amd.ops' public functions call torch.ops.feane
   feanet::residual_norm(u, f?, ktab?, pid?)           driver residual norm M-FEANet-mg_test.ipynb:27428
   feanet::pbc_pad(u, lo, hi)                          JacobiBlockPBC.pbc_boundary / reset_boundary
   feanet::jacobi_sweep_pbc(u, f, ktab, omd)           JacobiBlockPBC.jacobi_convolution FEANet/jacobi.py:86-97
+  feanet::mg_step(u, f, solver, cycles)               MultiGrid.Step / iterate (fused V-cycles of a
+                                                      MultigridSolver)  M-FEANet-mg_test.ipynb:27346-27372,
+                                                      FEANet/multigrid.py:159-185
 """
 from typing import Optional
 
@@ -191,3 +194,21 @@ def jacobi_sweep_pbc(u: Tensor, f: Tensor, ktab: Tensor, omd: Tensor) -> Tensor:
 @jacobi_sweep_pbc.register_fake
 def _(u, f, ktab, omd):
     return torch.empty_like(u, memory_format=torch.contiguous_format)
+
+
+@torch.library.custom_op("feanet::mg_step", mutates_args=(), device_types=_DEV)
+def mg_step(u: Tensor, f: Tensor, solver: int, cycles: int = 1) -> Tensor:
+    """`cycles` fused V-cycles of the MultigridSolver with handle `solver` (MultigridSolver.handle) from
+    the fine iterate u with right-hand side f; returns the new iterate [B, 1, H, W].  The solver's level
+    buffers, HIP graphs and schedule stay resident between calls: this op is the whole-cycle form of
+    MultiGrid.Step(v, f) (one pass per fused level kernel) that a notebook loop can call as
+    `u = torch.ops.feanet.mg_step(u, f, solver.handle)`."""
+    from .solver import solver_by_handle
+    return solver_by_handle(solver)._step(u, f, cycles)
+
+
+@mg_step.register_fake
+def _(u, f, solver, cycles=1):
+    from .solver import solver_by_handle
+    s = solver_by_handle(solver)
+    return u.new_empty((s.B, 1, s.H, s.W))

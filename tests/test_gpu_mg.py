@@ -849,6 +849,119 @@ def test_pipelined_state_semantics():
         assert torch.equal(a, b)
 
 
+def test_step_runs_unjoined_plan(monkeypatch):
+    """step() (MultiGrid.Step / iterate, one cycle from a loaded iterate, read at once) launches exactly the
+    unjoined plan — no cycle join, no discarded pipelined pre-smooth — also right after a pipelined
+    vcycle(k) call; and its result is bitwise the unjoined solver's."""
+    from feanet_amd import _lib
+    from feanet_amd.solver import MultigridSolver
+    n, B = 128, 2
+    rng = np.random.default_rng(5)
+    f = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    ref = MultigridSolver(n, dtype=torch.float64, batch=B, join_cycles=False).step(u0, f)
+    s = MultigridSolver(n, dtype=torch.float64, batch=B, graph=False)
+    names = []
+    real = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a: (names.append(name), real(name, *a))[1])
+    for warm in (False, True):
+        if warm:  # leave the solver in the pipelined state first
+            s.set_rhs(f=f)
+            s.load(u0)
+            s.vcycle(3)
+            s.solution()
+        names.clear()
+        out = s.step(u0, f)
+        torch.cuda.synchronize()
+        plan = [name for name, _ in s._plan("a")[0]]
+        body = [x for x in names if x not in ("mg_pack", "mg_unpack")]
+        assert body == plan, (warm, body)
+        assert "mg_cycle_join" not in names
+        assert names.count("mg_pack") == 3 and names.count("mg_unpack") == 1, names  # f, a, b; the result
+        assert torch.equal(out, ref)
+
+
+def test_set_boundary_takes_effect_at_load():
+    """set_boundary(new) followed by solution() / residual_norm() without a load(): the joined solver's
+    materialised end iterate carries the iterate buffers' (old) Dirichlet values, as the unjoined solver's."""
+    from feanet_amd.solver import MultigridSolver
+    n, B = 64, 1
+    rng = np.random.default_rng(8)
+    N = n + 1
+    f = torch.from_numpy(rng.standard_normal((B, 1, N, N))).cuda()
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, N, N))).cuda()
+    bc1 = torch.zeros(B, 1, N, N, dtype=torch.float64)
+    bc1[..., 0, :] = 1.0
+    bc2 = torch.zeros_like(bc1)
+    bc2[..., :, 0] = -2.0
+    out = []
+    for join in (False, True):
+        s = MultigridSolver(n, dtype=torch.float64, batch=B, join_cycles=join)
+        s.set_rhs(f=f)
+        s.set_boundary(bc1.cuda())
+        s.load(u0)
+        s.vcycle(3)
+        s.set_boundary(bc2.cuda())
+        out.append((s.solution(), s.residual_norm()))
+        s.load(u0)  # now bc2
+        s.vcycle(2)
+        out.append((s.solution(), s.residual_norm()))
+    (u_a, r_a), (u_a2, r_a2), (u_b, r_b), (u_b2, r_b2) = out
+    assert torch.equal(u_a, u_b) and torch.equal(r_a, r_b)
+    assert torch.equal(u_a2, u_b2) and torch.equal(r_a2, r_b2)
+    assert torch.equal(u_b[..., 0, 1:-1].cpu(), bc1[..., 0, 1:-1])
+    assert torch.equal(u_b2[..., :, 0].cpu(), bc2[..., :, 0])
+
+
+def test_mg_step_custom_op():
+    """torch.ops.feanet.mg_step (the fused V-cycle as a custom op): opcheck-clean, bitwise the solver's own
+    cycles, one and several per call."""
+    from feanet_amd import torch_ops  # noqa: F401
+    from feanet_amd.solver import MultigridSolver
+    n, B = 64, 2
+    rng = np.random.default_rng(9)
+    f = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    s = MultigridSolver(n, dtype=torch.float64, batch=B)
+    ref = MultigridSolver(n, dtype=torch.float64, batch=B, join_cycles=False)
+    for cyc in (1, 3):
+        got = torch.ops.feanet.mg_step(u0, f, s.handle, cyc)
+        ref.set_rhs(f=f)
+        ref.load(u0)
+        ref.vcycle(cyc)
+        assert torch.equal(got, ref.solution())
+        torch.library.opcheck(torch.ops.feanet.mg_step, (u0, f, s.handle, cyc),
+                              test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+    with pytest.raises(RuntimeError, match="no live MultigridSolver"):
+        torch.ops.feanet.mg_step(u0, f, 10 ** 9, 1)
+
+
+def test_multigrid_iterate_grad_mode_fused():
+    """FEANet/multigrid.py MultiGrid.iterate under autograd: the fused forward (bitwise the no-grad call)
+    with gradients from the recomputed module-level cycle — equal to back-propagating the module path."""
+    import FEANet.multigrid as mgm
+    lin = torch.asarray([[1, 2, 1], [2, 4, 2], [1, 2, 1]], dtype=torch.float32)
+    torch.set_default_device("cuda")
+    try:
+        mg = mgm.MultiGrid(32, lin / 16.0, lin / 4.0, torch.tensor([4.0, 1.0]))
+        g = torch.Generator(device="cuda").manual_seed(3)
+        f = torch.randn(2, 1, 33, 33, generator=g, device="cuda")
+        u = torch.randn(2, 1, 33, 33, generator=g, device="cuda")
+        with torch.no_grad():
+            v_ng = mg.iterate(u, f)
+        v = mg.iterate(u, f)
+        assert v.requires_grad and torch.equal(v.detach(), v_ng)
+        (v ** 2).sum().backward()
+        gR, gP = mg.conv.net.weight.grad.clone(), mg.deconv.net.weight.grad.clone()
+        mg.zero_grad()
+        vm = mg.iterate_modules(u, f)
+        (vm ** 2).sum().backward()
+    finally:
+        torch.set_default_device("cpu")
+    for a, b in ((gR, mg.conv.net.weight.grad), (gP, mg.deconv.net.weight.grad)):
+        assert (a - b).abs().max() <= 1e-4 * b.abs().max()
+
+
 ZVARIANT_ENV = ("FEANET_ZR_OVL", "FEANET_PZ_OVL", "FEANET_PZ_OVL_BYTES", "FEANET_PZ_BIG")
 
 

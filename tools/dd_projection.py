@@ -1,0 +1,128 @@
+"""Per-rank projection of the domain-decomposed V-cycle on ONE GPU.
+
+For a global grid split over P ranks (Pr x Pc blocks), one rank's whole program — its distributed levels
+0 .. Ld-1 with their ghost lines, the agglomeration copies and the redundant coarse sub-cycle (levels >= Ld
+of the global grid) — runs on this GPU with a communicator that moves nothing (NullComm): the time per
+V-cycle is that rank's kernel time, i.e. the N-GPU cycle time without communication.  The rank with the
+most ghost lines (an interior block) bounds the cycle.  Reported per Ld beside the single-GPU solver on the
+same global grid, so the agglomeration level can be chosen from measurements.
+
+GPU box:  python tools/dd_projection.py [--n 8192] [--steps 50] [--ld 3,4,5,6] [--out FILE.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "multigrid-feanet_amd"))
+import torch  # noqa: E402
+
+from feanet_amd.dd import DDSolver, default_grid, default_agglomeration, global_levels  # noqa: E402
+from feanet_amd.solver import MultigridSolver  # noqa: E402
+
+
+class NullComm:
+    """A communicator that moves nothing: exchanges and the all-gather are no-ops, the all-reduce is the
+    identity.  Only for timing one rank's kernels (values are not those of a real decomposition)."""
+    gpu = True
+
+    def exchange_many(self, s, items, wait=True):
+        return None
+
+    def exchange(self, s, l, name, d):
+        return None
+
+    def exchange_finish(self, handle):
+        return None
+
+    def allgather(self, target, source):
+        return None
+
+    def allreduce_sum(self, t):
+        return t
+
+
+def time_cycles(vcycle, steps, reps=3):
+    for _ in range(4):  # eager run + graph capture of every chunk, then warm replays
+        vcycle(steps)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        vcycle(steps)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / steps
+        best = t if best is None else min(best, t)
+    return best
+
+
+def interior_rank(Pr, Pc):
+    """A rank with the most neighbours (ghost lines on every side it can have)."""
+    ri = 1 if Pr > 2 else 0
+    ci = 1 if Pc > 2 else 0
+    return ri * Pc + ci
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--ranks", default="2,4,8")
+    ap.add_argument("--ld", default=None, help="agglomeration levels to try (default: default-1 .. default+2)")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    n = args.n
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    f = torch.randn(1, 1, n + 1, n + 1, dtype=torch.float64, device="cuda", generator=g)
+    single = MultigridSolver(n, dtype=torch.float64)
+    single.set_rhs(f=f)
+    single.load()
+    t1 = time_cycles(single.vcycle, args.steps)
+    print(f"single GPU {n + 1}^2: {t1 * 1e6:.1f} us per V-cycle", flush=True)
+    del single
+    torch.cuda.empty_cache()
+    rec = {"n": n, "single_gpu_us": t1 * 1e6, "ranks": {}}
+    L = global_levels(n, n)
+    for P in (int(x) for x in args.ranks.split(",")):
+        Pr, Pc = default_grid(P)
+        r = interior_rank(Pr, Pc)
+        d = default_agglomeration(n, n, Pr, L, Pc=Pc)
+        lds = [int(x) for x in args.ld.split(",")] if args.ld else [x for x in range(d - 1, d + 3) if 1 <= x <= L - 2]
+        rec["ranks"][P] = {"grid": f"{Pr}x{Pc}", "rank": r, "default_ld": d, "ld": {}}
+        for Ld in lds:
+            try:
+                s = DDSolver(n, n, r, P, comm=NullComm(), agglomerate=Ld, grid=(Pr, Pc))
+            except ValueError as e:
+                print(f"P={P} {Pr}x{Pc} Ld={Ld}: not partitionable ({e})", flush=True)
+                continue
+            s.set_rhs(f)
+            s.load()
+            t = time_cycles(s.vcycle, args.steps)
+            c = s.coarse
+            c.set_rhs(f=torch.randn(1, 1, c.H, c.W, dtype=torch.float64, device="cuda", generator=g))
+
+            def coarse_only(k):
+                for _ in range(k):
+                    c.load()
+                    c._vcycles_plain(1)
+            tc = time_cycles(coarse_only, args.steps)
+            p0, q0 = s.parts[0], s.cparts[0]
+            info = {"us_per_cycle": t * 1e6, "coarse_subcycle_us": tc * 1e6,
+                    "local_fine": f"{p0.Hloc}x{q0.Hloc}", "ghost0": s.part.ghost(0), "depths": list(s.depths),
+                    "coarse_grid": f"{c.H}x{c.W}", "projected_speedup": t1 / t}
+            rec["ranks"][P]["ld"][Ld] = info
+            print(f"P={P} {Pr}x{Pc} rank {r} Ld={Ld}: {t * 1e6:7.1f} us per cycle (coarse sub-cycle {tc * 1e6:5.1f} "
+                  f"us on {c.H}x{c.W}; local fine {p0.Hloc}x{q0.Hloc}, ghost {s.part.ghost(0)}), speed-up "
+                  f"{t1 / t:.2f} (no communication)", flush=True)
+            del s, c
+            torch.cuda.empty_cache()
+    if args.out:
+        json.dump(rec, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 # A/B of the fine-level kernels between the in-tree library and variant libraries (GPU box):
 #   bash tools/lab/ab_kernels.sh tools/lab/libB.so [tools/lab/libC.so ...]
 # Alternates processes A, B, ... three times each; each prints per-kernel times (kern_mix.py).

@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; T=gpurun_out/tail2; mkdir -p $T
 timeout -k 10 120 python tools/lab/tail_lab.py > $T/tail.txt 2>&1 || { cat $T/tail.txt; exit 1; }

@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 # Kernel-trace A/B of the V-cycle between the in-tree library and tools/lab/lib_old.so (GPU box):
 #   bash tools/lab/gpu_trace_ab.sh TAG [bench args]
 set -o pipefail

@@ -5,8 +5,7 @@ cd ${GRAFT_REPO_ROOT:-.}; export TMPDIR=/tmp; T=gpurun_out/$1; shift; mkdir -p $
 i=0
 for L in "$@"; do
   i=$((i+1))
-  if [ "$L" = "-" ]; then unset FEANET_LIB_OVERRIDE; else export FEANET_LIB_OVERRIDE=$L; fi
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $T/v$i -o run -- python3 bench.py --steps 300 --warmup 5 --no-cpu-baseline --kernel-reps 2 $BENCH_ARGS > $T/v$i.json 2> $T/v$i.err || { tail $T/v$i.err; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $T/v$i -o run -- python3 tools/lab/with_lib.py $L bench.py --steps 300 --warmup 5 --no-cpu-baseline --kernel-reps 2 $BENCH_ARGS > $T/v$i.json 2> $T/v$i.err || { tail $T/v$i.err; exit 1; }
   python3 tools/trace_summary.py $T/v$i > $T/v$i.txt
   echo "== [$L] $(python3 -c "import json; print(json.load(open('$T/v$i.json'))['ms_per_step']*1e3)") us"; head -${NLINES:-9} $T/v$i.txt
 done

@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 """Per-workgroup start/end and per-phase times (s_memrealtime, 100 MHz) of the multi-level launches:
 builds the whole library with -DFEA_MID_TRACE into tools/lab/mid_trace.so, runs mid_down / mid_up at
 513^2 (k = 3) and prints the workgroup start/end spread and workgroup 0's phase times.

@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 """Per-wave start / end of the level-1 residual-restriction kernel (2049^2 fp64, zero-guess) from a
 lab build with -DFEA_RR_TRACE (s_memrealtime, 10 ns ticks): is the launch dispatch-, latency- or
 tail-bound?  Build: python multigrid-feanet_amd/feanet_amd/build.py --out=tools/lab/lib_rrtrace.so -DFEA_RR_TRACE

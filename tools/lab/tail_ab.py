@@ -1,3 +1,4 @@
+# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 """Bitwise A/B of two library builds on V-cycles that use the coarse tail (run once per build,
 FEANET_LIB_OVERRIDE selects the build; the second run compares against the first's saved output).
 usage: python tools/lab/tail_ab.py OUT.npz [REF.npz]"""
