@@ -252,7 +252,7 @@ struct MgArgs {
   int rb;            // fine rows per row task (even)
   int rlo, rhi;      // row range of the residual norm
   int clo, chi;      // column range of the residual norm
-  int nt;            // nontemporal stores (level larger than FEANET_NT_BYTES)
+  int nt;            // 1: nontemporal stores (level larger than FEANET_NT_BYTES); 2: also loads (sweep, join)
 };
 
 struct TaskId {
@@ -359,12 +359,10 @@ __device__ __forceinline__ void store_masked(T* p, const T (&o)[V], int cl, int 
 // ---------------------------------------------------------------------------
 // Kernel A: interior Jacobi sweep  out = J(u, f);  ZERO: u == 0  ->  out = omd * f
 // ---------------------------------------------------------------------------
-// FEA_SWEEP_NTL (lab A/B): nontemporal loads of u and f on levels above the NT threshold
-#ifndef FEA_SWEEP_NTL
-#define FEA_SWEEP_NTL 0
-#endif
-constexpr bool kSweepNTL = FEA_SWEEP_NTL != 0;
-template <typename T, bool MULTI, bool ZERO, bool NT>
+// NTL: nontemporal loads of u and f too — on fields larger than the Infinity Cache (nt_policy: nothing of
+// them can be re-read from it; 8193^2 fp64 sweep 321 -> 310 us, 256 x 1025^2 fp32 700 -> 667 us, same-process
+// A/B, profiles/r03_stream/ntl_ab.txt; at 4097^2 it costs 64 -> 78 us, the fields being partly resident)
+template <typename T, bool MULTI, bool ZERO, bool NT, bool NTL = false>
 __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
   using F = Frame<T>;
   constexpr int V = F::VEC;
@@ -401,7 +399,7 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
     for (int r = r0; r < r1; ++r) {
       const long long ro = rowo(r) + V * lane;
       T fv[V], o[V];
-      vload<T, V>(fb + ro, fv);
+      vload<T, V, NTL>(fb + ro, fv);
       int pv[V];
       if constexpr (MULTI) pload<V>(pb + ro, pv);
 #pragma unroll
@@ -409,11 +407,11 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
       store_masked<T, V, NT>(ob + ro, o, cl, W);
     }
   } else {
-    Row<T, V> w0 = finish(raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0 - 1), lane));
-    Row<T, V> w1 = finish(raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0), lane));
-    RawRow<T, V> nx = raw_row<T, V, kSweepNTL && NT>(ub + rowo(r0 + 1), lane);
+    Row<T, V> w0 = finish(raw_row<T, V, NTL>(ub + rowo(r0 - 1), lane));
+    Row<T, V> w1 = finish(raw_row<T, V, NTL>(ub + rowo(r0), lane));
+    RawRow<T, V> nx = raw_row<T, V, NTL>(ub + rowo(r0 + 1), lane);
     T fx[V];
-    vload<T, V, kSweepNTL && NT>(fb + rowo(r0) + V * lane, fx);
+    vload<T, V, NTL>(fb + rowo(r0) + V * lane, fx);
     PRow<V> p0{}, p1{}, p2{};
     RawP<V> px{};
     if constexpr (MULTI) {
@@ -423,9 +421,9 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
     }
     for (int r = r0; r < r1; ++r) {
       // issue next iteration's loads before this row's arithmetic
-      const RawRow<T, V> nn = raw_row<T, V, kSweepNTL && NT>(ub + rowo(r + 2), lane);
+      const RawRow<T, V> nn = raw_row<T, V, NTL>(ub + rowo(r + 2), lane);
       T fn[V];
-      vload<T, V, kSweepNTL && NT>(fb + rowo(r + 1) + V * lane, fn);
+      vload<T, V, NTL>(fb + rowo(r + 1) + V * lane, fn);
       RawP<V> pn{};
       if constexpr (MULTI) pn = raw_prow<V>(pb + rowo(r + 2), lane);
       const Row<T, V> w2 = finish(nx);
@@ -1579,11 +1577,9 @@ static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of
 #define FEA_JOIN_NTL 1
 #endif
 constexpr bool kJoinNTL = FEA_JOIN_NTL != 0;
-// FEA_JOIN_NTF (lab A/B): nontemporal loads of the right-hand side f too
-#ifndef FEA_JOIN_NTF
-#define FEA_JOIN_NTF 0
-#endif
-constexpr bool kJoinNTF = FEA_JOIN_NTF != 0;
+// NTF (template flag of the join): nontemporal loads of the right-hand side f too, on levels whose fields of
+// ONE sample exceed the Infinity Cache (8193^2 fp64 join 397 -> 371 us; with many small samples, C5, it
+// costs 953 -> 980 us; same-process A/B, profiles/r03_stream/ntl_ab.txt)
 // FEA_JOIN_ALT: odd row tasks stream bottom-up (see join_task).  FEA_JOIN_SHARED: the rows two tasks
 // share are loaded through the cache instead of nontemporally (with FEA_JOIN_NTL).  Same-lease A/B at
 // 4097^2 fp64 (profiles/r02_ab): ALT=1 join 82.6 us, 348 MB read per launch; ALT=0 84.3 us, 385 MB;
@@ -1617,7 +1613,7 @@ struct Ovl3 {
 // traffic per launch at 4097^2 fp64, measured; nontemporal loads still allocate there).  Every node value
 // is the same expression as in the forward task: windows are passed to the stencil in grid order and
 // a coarse row's three restriction terms are summed in the forward order (ky = 0, 1, 2).
-template <typename T, bool MULTI, bool NT, bool NORM, bool REV>
+template <typename T, bool MULTI, bool NT, bool NORM, bool REV, bool NTF>
 __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* rtb,
                                           const T* ptb, double& ssq) {
   constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
@@ -1705,7 +1701,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
 #pragma unroll
   for (int q = 0; q < kJoinAhead; ++q) {
     load_u(yb + S * q, ub_[q]);
-    vload<T, V, kJoinNTF && NT>(fb + rowo(yb + S * (q - 1)), fb_[q]);
+    vload<T, V, NTF>(fb + rowo(yb + S * (q - 1)), fb_[q]);
     if constexpr (MULTI) pload<V>(pb + rowo(yb + S * q), pb_[q]);
   }
   // coarse rows: Ca = the row an even step uses, Cb = the next one in streaming order
@@ -1754,7 +1750,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
       if constexpr (MULTI) p0[k] = bp[k];
     }
     load_u(y + S * kJoinAhead, bu);
-    vload<T, V, kJoinNTF && NT>(fb + rowo(y + S * (kJoinAhead - 1)), bf);
+    vload<T, V, NTF>(fb + rowo(y + S * (kJoinAhead - 1)), bf);
     if constexpr (MULTI) pload<V>(pb + rowo(y + S * kJoinAhead), bp);
     // 1. x(y) = u(y) + w1 P(ec) on the own columns (correct_even / correct_odd of Kernel C)
     T x[V];
@@ -1906,7 +1902,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   }
 }
 
-template <typename T, bool MULTI, bool NORM, bool NT>
+template <typename T, bool MULTI, bool NORM, bool NT, bool NTF = false>
 __global__ __launch_bounds__(256)
 #if FEA_JOIN_WAVES > 0
 __attribute__((amdgpu_waves_per_eu(FEA_JOIN_WAVES)))
@@ -1923,8 +1919,8 @@ void k_mg_cycle_join(MgArgs<T> g) {
   const TaskId id = decode_task_lin(g.nstrips, g.ntr);
   double ssq = 0.0;
   if (id.valid) {
-    if (kJoinAlternate && (id.t & 1)) join_task<T, MULTI, NT, NORM, true>(g, id, tab, rtb, ptb, ssq);
-    else join_task<T, MULTI, NT, NORM, false>(g, id, tab, rtb, ptb, ssq);
+    if (kJoinAlternate && (id.t & 1)) join_task<T, MULTI, NT, NORM, true, NTF>(g, id, tab, rtb, ptb, ssq);
+    else join_task<T, MULTI, NT, NORM, false, NTF>(g, id, tab, rtb, ptb, ssq);
   }
   if constexpr (NORM) norm_partial<T>(g, ssq);
 }
@@ -2099,6 +2095,11 @@ static long long nt_bytes() {
   return e ? atoll(e) : (64ll << 20);
 }
 
+// Fields larger than the 256 MiB Infinity Cache cannot be re-read from it between launches: there the sweep
+// and (for one sample's field) the cycle join also load nontemporally (g.nt = 2, see k_mg_sweep / the join).
+// Tied to the store threshold (4 x 64 MiB by default) so the tests' FEANET_NT_BYTES=0 runs both paths.
+static long long nt_load_bytes() { return 4 * nt_bytes(); }
+
 // zero-guess residual-restriction without a kept v on overlapped strips (k_mg_zero_restrict; bitwise the
 // per-lane-halo kernel, which FEANET_ZR_OVL=0 selects for A/B)
 static bool zero_ovl() {
@@ -2232,6 +2233,14 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     else K<TARGS, false><<<grid, 256, 0, s>>>(g);                 \
   }
 
+// three streaming policies (g.nt: 0 cached, 1 nontemporal stores, 2 also nontemporal loads)
+#define FEA_NT3_LAUNCH(K, TARGS)                                  \
+  {                                                               \
+    if (g.nt == 2) K<TARGS, true, true><<<grid, 256, 0, s>>>(g);  \
+    else if (g.nt) K<TARGS, true, false><<<grid, 256, 0, s>>>(g); \
+    else K<TARGS, false, false><<<grid, 256, 0, s>>>(g);          \
+  }
+
 #define FEA_NT_LAUNCH_ZU(K, TARGS)                                \
   {                                                               \
     if (g.nt) K<TARGS, true, true><<<grid, 256, 0, s>>>(g);       \
@@ -2260,15 +2269,16 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || out == u) return FEA_EINVAL;             \
     MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
     g.u = u; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;                   \
+    if (g.nt && (long long)B * bs * (long long)sizeof(T) > nt_load_bytes()) g.nt = 2;                      \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (!u) {                                                                                                \
-      if (multi) FEA_NT_LAUNCH(k_mg_sweep, T COMMA true COMMA true)                                          \
-      else FEA_NT_LAUNCH(k_mg_sweep, T COMMA false COMMA true)                                               \
+      if (multi) FEA_NT3_LAUNCH(k_mg_sweep, T COMMA true COMMA true)                                          \
+      else FEA_NT3_LAUNCH(k_mg_sweep, T COMMA false COMMA true)                                               \
     } else {                                                                                                 \
-      if (multi) FEA_NT_LAUNCH(k_mg_sweep, T COMMA true COMMA false)                                         \
-      else FEA_NT_LAUNCH(k_mg_sweep, T COMMA false COMMA false)                                              \
+      if (multi) FEA_NT3_LAUNCH(k_mg_sweep, T COMMA true COMMA false)                                         \
+      else FEA_NT3_LAUNCH(k_mg_sweep, T COMMA false COMMA false)                                              \
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
@@ -2423,17 +2433,18 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;     \
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     join_config<T>(B, H, W, g);                                                                              \
+    if (g.nt && bs * (long long)sizeof(T) > nt_load_bytes()) g.nt = 2;                                         \
     g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
     hipStream_t s = (hipStream_t)stream;                                                                     \
     if (norm && (long long)grid.x * kWaves * 8 > (long long)fea_norm_workspace_bytes(B, H, W))               \
       return FEA_EINVAL;                                                                                     \
     if (multi) {                                                                                             \
-      if (norm) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true COMMA true)                                      \
-      else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA true COMMA false)                                          \
+      if (norm) FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA true COMMA true)                                      \
+      else FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA true COMMA false)                                          \
     } else {                                                                                                 \
-      if (norm) FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA true)                                     \
-      else FEA_NT_LAUNCH(k_mg_cycle_join, T COMMA false COMMA false)                                         \
+      if (norm) FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA false COMMA true)                                     \
+      else FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA false COMMA false)                                         \
     }                                                                                                        \
     if (append)                                                                                              \
       k_norm_append<<<1, 256, 0, s>>>(norm_ws, 0, (long long)(grid.x / B) * kWaves, B, 1, norm_hist, norm_cnt); \
