@@ -49,12 +49,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_init(force=False):
+def dist_init(force=False, backend="nccl"):
     """One process per GPU (torchrun env).  force: create the process group even for one rank (the
-    domain-decomposed path always talks through torch.distributed)."""
+    domain-decomposed path always talks through torch.distributed).  backend "gloo": rehearsal of the
+    multi-rank path with several processes on one GPU (RCCL refuses two ranks on one device)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":  # rehearsal: more ranks than GPUs share them
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if ws > 1 or force:
         import torch.distributed as dist
@@ -62,7 +65,10 @@ def dist_init(force=False):
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(ws))
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return ws, rank
 
 
@@ -76,7 +82,7 @@ def max_over_ranks(x, ws):
     if ws == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -234,6 +240,29 @@ def cpu_baseline(n, seconds_budget=16.0):
                                      "sample": f"{kn} V-cycles (median {tn:.2f} s) by oracle/feanet_oracle.py"}}
 
 
+def single_gpu_same_grid(m, n, T, B, steps, ms_dd):
+    """The single-GPU MultigridSolver on the decomposed run's global grid ((m+1) x (n+1), same seeded rhs),
+    timed like the main line (warm-up calls, then one vcycle(steps) between synchronisations)."""
+    from feanet_amd.solver import MultigridSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    s = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B)
+    s.set_rhs(f=torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g))
+    s.load()
+    for _ in range(6):
+        s.vcycle(steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(steps)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    del s
+    torch.cuda.empty_cache()
+    return {"ms_per_step": t * 1e3, "value": B * (m + 1) * (n + 1) / t, "unit": "DoF-updates/s",
+            "speedup_of_this_line": t * 1e3 / ms_dd,
+            "workload": f"{m + 1}x{n + 1} poisson V-cycle on one GPU (MultigridSolver, no decomposition), rank 0"}
+
+
 def dd_domain(P, n0):
     """Weak-scaled global grid for P slabs of n0 x n0 intervals each, aspect ratio <= 2 when P is a
     power of two: 1 -> n0 x n0, 2 -> 2n0 x n0, 4 -> 2n0 x 2n0, 8 -> 4n0 x 2n0 (rows x columns)."""
@@ -271,12 +300,14 @@ def main():
                          "families of the reference's Data/RHS/generate_rhs.py with FNet applied (default: "
                          "families for batches, the BASELINE C5 inputs; randn otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend (gloo: multi-process rehearsal on one GPU, host-staged)")
     ap.add_argument("--kernel-reps", type=int, default=50)
     args = ap.parse_args()
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     mode = args.mode or ("dd" if ws > 1 else "single")
-    ws, rank = dist_init(force=(mode == "dd"))
+    ws, rank = dist_init(force=(mode == "dd"), backend=args.backend)
     from feanet_amd.solver import MultigridSolver
     T = torch.float64 if args.dtype == "f64" else torch.float32
     n, B = args.n, args.batch
@@ -410,6 +441,12 @@ def main():
         "vcycle_algorithmic_bytes": vbytes,
         "residual_contraction_per_cycle": conv,
     }
+    if mode == "dd" and ws > 1:
+        # the same global grid on ONE GPU (rank 0; the others wait at the barrier): the strong-scaling base
+        # point of this line, so speed-up and efficiency follow from the line itself
+        if rank == 0:
+            rec["single_gpu_same_grid"] = single_gpu_same_grid(m, nc, T, B, args.steps, ms_step)
+        barrier(ws)
     if rank == 0 and ws == 1 and mode == "single" and not args.no_cpu_baseline and args.problem == "poisson" \
             and B == 1:
         log("[bench] timing the CPU oracle baseline ...")

@@ -684,16 +684,6 @@ struct Ovl {
   static constexpr int S = ((63 * V - 3) / V) * V;  // owned fine columns per strip (mult. of V)
   static constexpr int OWN = S / V;                 // owning lanes: 1 .. OWN
 };
-// owned strips of whole 128-byte lines (lanes 1..56 own, 57..63 only feed their neighbours): for kernels
-// whose fine-level STORES dominate, so no line is written by two waves
-template <typename T>
-struct OvlA {
-  static constexpr int V = Frame<T>::VEC;
-  static constexpr int S = 56 * V;
-  static constexpr int OWN = S / V;
-  static_assert(S % Frame<T>::A == 0, "line-aligned owned strips");
-};
-
 template <typename T, int V>
 __device__ __forceinline__ Row<T, V> own_row(const T (&x)[V]) {  // window L, own.., R from own values
   Row<T, V> w;
@@ -1357,10 +1347,10 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 // Lanes 1..OWN store.  Same per-node expressions (crow_term, correction order, sweep) as k_mg_prolong,
 // so the output is bitwise the same.
 // ---------------------------------------------------------------------------
-template <typename T, bool MULTI, bool ALIGN, bool NT>
+template <typename T, bool MULTI, bool NT>
 __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
   using F = Frame<T>;
-  using O = std::conditional_t<ALIGN, OvlA<T>, Ovl<T>>;
+  using O = Ovl<T>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
@@ -2029,13 +2019,11 @@ static inline bool mg_dim_ok(int n) { return n >= 3 && n <= (1 << 20) + 1; }
 static inline bool mg_dims_ok(int H, int W) { return mg_dim_ok(H) && mg_dim_ok(W); }
 static inline bool mg_odd(int H, int W) { return (H & 1) && (W & 1); }
 
-// Rows per wave task: the largest even count (<= kRB) that still gives >= target waves, so small
-// levels are spread over the chip instead of being marched row by row by a few waves.
-// (tuning knobs are read at every launch so one process can A/B them; graphs capture the choice)
-static int target_waves() {
-  const char* e = getenv("FEANET_TARGET_WAVES");  // default 2048 = 8 waves per CU
-  return e ? std::max(64, atoi(e)) : 2048;
-}
+// Rows per wave task: the largest even count (<= kRB) that still gives >= kTargetWaves waves, so small
+// levels are spread over the chip instead of being marched row by row by a few waves (1024 / 4096 / 8192
+// measured slower than 2048 on levels 1-2, profiles/r02_ab).
+constexpr int kTargetWaves = 2048;  // 8 waves per CU
+static int target_waves() { return kTargetWaves; }
 static inline int pick_rb(int B, int nstrips, int rows, int maxrb = kRB) {
   const int tw = target_waves();
   for (int rb = maxrb; rb > 2; rb /= 2)
@@ -2059,15 +2047,12 @@ static int num_cus() {
 // workgroups run a few per CU at once: choose the task height so the workgroup count fills the CUs
 // evenly (ceil(WGs / CUs) decides the slowest CU), counting the `halo` rows each task re-streams,
 // with at least target_waves() waves in flight.  e.g. 4097^2 fp64: 504 workgroups of 74 rows
-// (2 per CU) instead of 576 of 64 (2.25 per CU: a quarter of the CUs run 3).  FEANET_BALANCE=0
-// restores the power-of-two choice (A/B).  Results are bitwise independent of the task height.
-static int rb_occ() {
-  const char* e = getenv("FEANET_RB_OCC");
-  return e ? atoi(e) : 0;
-}
+// (2 per CU) instead of 576 of 64 (2.25 per CU: a quarter of the CUs run 3).  Results are bitwise
+// independent of the task height.  Same-process A/B against the power-of-two height
+// (profiles/r03_stream/balance_ab.txt): join -13.5 % at 4097^2, -3 % at 8193^2, -6 % on C3, -11 % at 2049^2
+// fp32; sweep+restriction -2 .. -12 %.  Batches of many samples are the exception (cycle_join_rb).
 static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
-  const char* e = getenv("FEANET_BALANCE");
-  if ((e && atoi(e) == 0) || rows_c < 2) return rb_pow2;
+  if (rows_c < 2) return rb_pow2;
   const long long ncu = num_cus();
   const long long min_wg = std::max<long long>(1, target_waves() / kWaves);
   long long best_cost = -1;
@@ -2075,9 +2060,7 @@ static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
   for (int rbc = 1; rbc <= rows_c && 2 * rbc <= 4 * rb_pow2; ++rbc) {
     const long long ntr = div_up(rows_c, rbc), wgs = (long long)B * div_up(ntr * nstrips, kWaves);  // linear order
     if (wgs < min_wg) break;  // larger tasks only lower the count further
-    // FEANET_RB_OCC = k > 0: cost by rounds of k resident workgroups per CU (A/B knob)
-    const long long occ = rb_occ();
-    const long long cost = (occ > 0 ? div_up(wgs, ncu * occ) * occ : div_up(wgs, ncu)) * (2 * rbc + halo);
+    const long long cost = div_up(wgs, ncu) * (2 * rbc + halo);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
       best = 2 * rbc;
@@ -2100,36 +2083,18 @@ static long long nt_bytes() {
 // Tied to the store threshold (4 x 64 MiB by default) so the tests' FEANET_NT_BYTES=0 runs both paths.
 static long long nt_load_bytes() { return 4 * nt_bytes(); }
 
-// zero-guess residual-restriction without a kept v on overlapped strips (k_mg_zero_restrict; bitwise the
-// per-lane-halo kernel, which FEANET_ZR_OVL=0 selects for A/B)
-static bool zero_ovl() {
-  const char* e = getenv("FEANET_ZR_OVL");
-  return !(e && atoi(e) == 0);
-}
-
-// prolongation + sweep of a recomputed zero-guess iterate on overlapped strips (k_mg_prolong_zu_ovl; bitwise
-// k_mg_prolong<ZU>) on levels of at most FEANET_PZ_OVL_BYTES (default 16 MiB): there the shorter per-wave
-// chain pays (1025^2 fp64: 6.1 -> 5.5 us); on larger levels the fine output dominates and the owned strips
-// (122 of 128 columns) split 128-byte lines between two waves' stores (2049^2: 14.6 -> 15.0 us, same-lease
-// A/B, profiles/r02_ab/prolong_ovl).  FEANET_PZ_OVL=0 turns it off.
-// Larger levels: FEANET_PZ_BIG = 0 keeps k_mg_prolong<ZU>, 1 the same overlapped strips, 2 line-aligned owned
-// strips (OvlA).  Returns 0 (k_mg_prolong<ZU>), 1 (Ovl) or 2 (OvlA).
-static int zu_ovl(long long level_bytes) {
-  const char* e = getenv("FEANET_PZ_OVL");
-  if (e && atoi(e) == 0) return 0;
-  const char* b = getenv("FEANET_PZ_OVL_BYTES");
-  if (level_bytes <= (b ? atoll(b) : (16ll << 20))) return 1;
-  const char* big = getenv("FEANET_PZ_BIG");
-  const int m = big ? atoi(big) : 0;
-  return (m >= 0 && m <= 2) ? m : 0;
-}
+// Prolongation + sweep of a recomputed zero-guess iterate (levels >= 1 going up): on overlapped strips
+// (k_mg_prolong_zu_ovl, bitwise k_mg_prolong<ZU>) on levels of at most a quarter of the nontemporal-store
+// threshold (16 MiB by default): there the shorter per-wave chain pays (1025^2 fp64: 6.1 -> 5.5 us); on
+// larger levels the fine output dominates and the owned strips (122 of 128 columns) split 128-byte lines
+// between two waves' stores (2049^2: 14.6 -> 15.0 us; line-aligned owned strips of 112 columns: no gain;
+// same-lease A/B, profiles/r02_ab/prolong_ovl).  Tied to FEANET_NT_BYTES so the tests' FEANET_NT_BYTES=0
+// runs select the other kernel on the same level (bitwise comparison of the two).
+static bool zu_ovl(long long level_bytes) { return level_bytes <= nt_bytes() / 4; }
 
 // rows per task cap of the cycle-join kernel (its stages recompute 7 rows per task)
-static int join_max_rb() {
-  const char* e = getenv("FEANET_JOIN_RB");
-  const int v = e ? atoi(e) : 64;
-  return (v >= 4 && (v & (v - 1)) == 0) ? v : 64;
-}
+constexpr int kJoinMaxRB = 64;
+static int join_max_rb() { return kJoinMaxRB; }
 
 template <typename T>
 static MgArgs<T> mg_args(int H, int W, int ld, long long bs, int B) {
@@ -2198,10 +2163,15 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
 }
 
 // launch configuration of the cycle join (overlapped strips, balanced row tasks)
+// Batches of >= 16 samples keep the power-of-two task height (64 rows): many short tasks balance better
+// than few long balanced ones there (256 x 1025^2 fp32 join 899 -> 843 us, 16 x 1025^2 59.4 -> 57.3 us;
+// 8 x 2049^2 fp64 prefers balanced, 201 vs 207 us; profiles/r03_stream/balance_ab.txt).
+constexpr int kJoinBatchPow2 = 16;
 template <typename T>
 static void join_config(int B, int H, int W, MgArgs<T>& g) {
   g.nstrips = div_up(W - 2, Ovl3<T>::S);
-  g.rb = balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, pick_rb(B, g.nstrips, H - 2, join_max_rb()));
+  const int rb_pow2 = pick_rb(B, g.nstrips, H - 2, join_max_rb());
+  g.rb = B >= kJoinBatchPow2 ? rb_pow2 : balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, rb_pow2);
   g.ntr = div_up((H + 1) / 2 - 2, g.rb / 2);
 }
 
@@ -2299,7 +2269,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     hipStream_t s = (hipStream_t)stream;                                                                     \
     const bool multi = ntab > 1;                                                                             \
     if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
-    if (!u && !v_out && zero_ovl()) { /* zero guess, v not kept: overlapped strips (k_mg_zero_restrict) */  \
+    if (!u && !v_out) { /* zero guess, v not kept: overlapped strips (k_mg_zero_restrict) */                \
       g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                  \
       g.rb = pick_rb(B, g.nstrips, H - 2);                                                                   \
       g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                    \
@@ -2373,19 +2343,13 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2;          \
     g.ldc = ldc; g.bsc = bsc;                                                                                \
     hipStream_t s = (hipStream_t)stream;                                                                     \
-    const int zm = (sweep && !u) ? zu_ovl((long long)B * bs * (long long)sizeof(T)) : 0;                    \
-    if (zm) { /* overlapped strips */                                                                        \
-      g.nstrips = div_up(W - 2, zm == 2 ? OvlA<T>::S : Ovl<T>::S);                                           \
+    if (sweep && !u && zu_ovl((long long)B * bs * (long long)sizeof(T))) { /* overlapped strips */           \
+      g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                  \
       g.rb = pick_rb(B, g.nstrips, H - 2);                                                                   \
       g.ntr = div_up(H - 2, g.rb);                                                                           \
       const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                    \
-      if (zm == 2) {                                                                                         \
-        if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true COMMA true)                               \
-        else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false COMMA true)                                    \
-      } else {                                                                                               \
-        if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true COMMA false)                              \
-        else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false COMMA false)                                   \
-      }                                                                                                      \
+      if (multi) FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA true)                                            \
+      else FEA_NT_LAUNCH(k_mg_prolong_zu_ovl, T COMMA false)                                                 \
       FEA_LAUNCH_CHECK();                                                                                    \
     }                                                                                                        \
     const dim3 grid = mg_grid(B, g.ntr, g.nstrips);                                                          \

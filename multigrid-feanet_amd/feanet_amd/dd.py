@@ -717,8 +717,9 @@ class TorchComm:
     """Halo exchange / all-gather / all-reduce over torch.distributed.  With the nccl backend (RCCL
     on ROCm) device buffers are sent directly; with gloo they are staged through host memory."""
 
-    def __init__(self, group=None):
-        import torch.distributed as dist
+    def __init__(self, group=None, dist=None):
+        if dist is None:  # (tests pass an in-process stand-in with the same interface)
+            import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.rank = dist.get_rank(group)

@@ -18,7 +18,6 @@ are the ones a caller asks for (e.g. `.item()` on the residual norm, as the refe
 """
 import itertools
 import math
-import os
 import time
 import weakref
 
@@ -119,7 +118,7 @@ class MultigridSolver:
             pre-smooth + residual + restriction of the next as one pass (fea_mg_cycle_join; bitwise
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
         mid: run latency-bound coarse levels (B*H*W <= MID_NODES) up to four per launch
-            (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels); env FEANET_MID=0 disables.
+            (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels).
     """
 
     MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
@@ -162,7 +161,7 @@ class MultigridSolver:
         self.fuse = fuse
         self.zero_start = zero_start
         self.join_cycles = join_cycles
-        self.mid = bool(mid) and os.environ.get("FEANET_MID", "1") != "0"
+        self.mid = bool(mid)
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -377,10 +376,6 @@ class MultigridSolver:
         times the top level's nodes."""
         esz = 4 if self.dtype == torch.float32 else 8
         multi = self.ntab > 1
-        if up and os.environ.get("FEANET_MID_UP_TILE"):  # A/B knob: "RxC" rows x columns of the up tiles
-            TR, TC = (int(x) for x in os.environ["FEANET_MID_UP_TILE"].lower().split("x"))
-            if _lib.mid_lds_bytes(up, k, TR, TC, esz, multi) > 0:
-                return (TR, TC)
         tl = self.levels[a if up else a + k]
         top = self.levels[a]
         best = None
@@ -399,7 +394,7 @@ class MultigridSolver:
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
-        cap = int(os.environ.get("FEANET_MID_UP_NODES", self.MID_NODES)) if up else self.MID_NODES
+        cap = self.MID_NODES
         el = sorted(l for l in levels
                     if self.B * self.levels[l].H * self.levels[l].W <= cap and l + 1 < self.L)
         groups = []
@@ -545,7 +540,7 @@ class MultigridSolver:
         prog.append((("tail", pre), mid + [tail]))
         return prog, other(pre)
 
-    GRAPH_CYCLES = int(os.environ.get("FEANET_GRAPH_CYCLES", "32"))  # max joined cycles per HIP graph
+    GRAPH_CYCLES = 32  # max joined cycles per HIP graph
 
     @staticmethod
     def graph_blocks(njoin, G):

@@ -297,7 +297,11 @@ def hnet(x, geo, weights):
 # A11-A14: V-cycles
 # ---------------------------------------------------------------------------
 class Level:
-    def __init__(self, n, problem="poisson", dtype=np.float32, prop=(1, 20), shape=0, omega=2. / 3., m=None):
+    """pids: optional {N: pattern map} of the two-material problem computed earlier by interface_mesh (the
+    element/node loops are O(N^2) Python: tests/golden/c3_pattern_maps.npz holds their output up to 2049^2)."""
+
+    def __init__(self, n, problem="poisson", dtype=np.float32, prop=(1, 20), shape=0, omega=2. / 3., m=None,
+                 pids=None):
         self.n = n
         self.m = n if m is None else m
         self.N = n + 1
@@ -305,6 +309,11 @@ class Level:
         self.dtype = dtype
         if problem == "poisson":
             self.ktab, self.pid = square_mesh((self.H, self.W))
+        elif pids is not None and self.N in pids:
+            assert self.m == n, "two-material problem: square only"
+            a = np.array(prop, np.float32)
+            self.ktab = np.stack([pattern_stencil(a, REF_PATTERNS[k]) for k in range(16)])
+            self.pid = np.asarray(pids[self.N], np.uint8)
         else:
             assert self.m == n, "two-material problem: square only"
             self.ktab, self.pid = interface_mesh(self.N, prop, shape)
@@ -330,11 +339,11 @@ class OracleMultigrid:
                MM_Interface_error.ipynb:141 (pre-smoothing applied to grids[0] at every depth)."""
 
     def __init__(self, n, problem="poisson", dtype=np.float32, levels=None, rtab=None, ptab=None,
-                 w=(1.0, 1.0), prop=(1, 20), shape=0, rows=None):
+                 w=(1.0, 1.0), prop=(1, 20), shape=0, rows=None, pids=None):
         self.n = n
         m = n if rows is None else rows
         self.L = int(np.log2(min(n, m))) if levels is None else levels
-        self.levels = [Level(n >> l, problem, dtype, prop, shape, m=m >> l) for l in range(self.L)]
+        self.levels = [Level(n >> l, problem, dtype, prop, shape, m=m >> l, pids=pids) for l in range(self.L)]
         lin = np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float32)
         nch = len(self.levels[0].ktab)
         self.rtab = (np.broadcast_to(lin / 4, (nch, 3, 3)) if rtab is None else np.asarray(rtab, np.float32))

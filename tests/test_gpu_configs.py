@@ -1,11 +1,12 @@
 """BASELINE.json configurations as GPU parity cases: each checked against the oracle or
 against the single-GPU path, at the configuration's own size.
   C2  1025^2 Poisson fp64, 6-level V-cycle                      -> oracle, every cycle, 1e-10
-  C3  2049^2 two-material, learned R/P ratio (multigrid.py)     -> oracle first cycle + convergence
+  C3  2049^2 two-material, learned R/P ratio (multigrid.py)     -> oracle, three cycles, 1e-10 + convergence
   C4  8193^2 Poisson fp64 over 8 ranks (slabs, 4 x 2 blocks)   -> bitwise the single-GPU V-cycle,
                                                                    which is checked against the oracle
   C5  256 x 1025^2 fp32 batch                                   -> bitwise per-sample independence,
-                                                                   oracle fp32 first cycle of 3 samples
+                                                                   oracle fp32 first cycle of 3 samples,
+                                                                   their residual norms over 3 cycles
 """
 import os
 
@@ -50,30 +51,29 @@ def test_c3_2049_interface_learned_ratio():
     s.set_rhs(F=F)
     s.load()
     r0 = float(s.residual_norm()[0])
-    s.vcycle()
-    got = s.solution().cpu().numpy()[:, 0]
     # oracle: same operators; pattern maps computed by the ORACLE's own element/node loop
     # (tests/golden/c3_pattern_maps.npz, made by tests/golden/make_c3_maps.py and re-checked against
     # the loop in the CPU suite, tests/test_setup.py::test_c3_maps_fixture_is_oracle)
     maps = np.load(os.path.join(HERE, "golden", "c3_pattern_maps.npz"))
-    mg = orc.OracleMultigrid(256, "poisson", np.float64)  # placeholder hierarchy, levels replaced below
-    mg.levels = []
-    for l in range(s.L):
-        lv = orc.Level(n >> l, "poisson", np.float64)
-        lv.ktab = maps["ktab"]
-        lv.pid = maps[f"pid_{(n >> l) + 1}"]
-        mg.levels.append(lv)
-    mg.L = s.L
-    mg.rtab = np.broadcast_to(np.asarray(w["R"][0], np.float32), (16, 3, 3))
-    mg.ptab = np.asarray(w["P"][:, 0], np.float32)
-    mg.w = tuple(float(x) for x in w["w"])
+    pids = {int(k[4:]): maps[k] for k in maps.files if k.startswith("pid_")}
+    mg = orc.OracleMultigrid(n, "interface", np.float64, levels=s.L, pids=pids,
+                             rtab=np.broadcast_to(np.asarray(w["R"][0], np.float32), (16, 3, 3)),
+                             ptab=np.asarray(w["P"][:, 0], np.float32), w=tuple(float(x) for x in w["w"]))
     f = orc.conv3x3(np.ones((1, n + 1, n + 1)), orc.fnet_stencil(2.0 / n))
-    v = mg.step(np.zeros((1, n + 1, n + 1)), f)
-    assert np.abs(got - v).max() / np.abs(v).max() < 1e-10
+    v = np.zeros((1, n + 1, n + 1))
+    # one plain V-cycle, then two joined ones (fea_mg_cycle_join with the two-material tables)
+    for k, cyc in enumerate((1, 2)):
+        s.vcycle(cyc)
+        for _ in range(cyc):
+            v = mg.step(v, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        assert np.abs(got - v).max() / np.abs(v).max() < 1e-10, k
+    res, ref = float(s.residual_norm()[0]), float(mg.residual_norm(v, f)[0])
+    assert abs(res - ref) <= 1e-9 * ref, (res, ref)
     # converges, slowly at this size (contrast 20, and the reference's coarsest level is two Jacobi
     # sweeps on 3^2), not strictly monotonically per cycle; over two cycles always
     r = [float(s.residual_norm()[0])]
-    for _ in range(15):
+    for _ in range(13):
         s.vcycle()
         r.append(float(s.residual_norm()[0]))
     assert all(b < a for a, b in zip(r, r[2:])), r
@@ -162,11 +162,21 @@ def test_c5_batch256_1025_fp32():
     s3 = MultigridSolver(n, dtype=torch.float32, batch=3)
     s3.set_rhs(f=f[idx])
     s3.load()
-    s3.vcycle()
     mg = orc.OracleMultigrid(n, "poisson", np.float32)
     fb = f[idx, 0].cpu().numpy()
-    v = mg.step(np.zeros_like(fb), fb)
-    got = s3.solution().cpu().numpy()[:, 0]
-    for i in range(3):
-        err = np.abs(got[i] - v[i]).max() / np.abs(v[i]).max()
-        assert err < 2e-5, (idx[i], err)
+    r0 = orc.interior_norm(fb - mg.levels[0].K(np.zeros_like(fb)))
+    v = np.zeros_like(fb)
+    for k in range(3):
+        s3.vcycle()
+        v = mg.step(v, fb)
+        if k == 0:
+            got = s3.solution().cpu().numpy()[:, 0]
+            for i in range(3):
+                err = np.abs(got[i] - v[i]).max() / np.abs(v[i]).max()
+                assert err < 2e-5, (idx[i], err)
+        # residual norms of every cycle to 1 % + 1e-3 of the initial residual: with these smooth sources r is a
+        # small difference of large K u terms, and two fp32 implementations' iterates differ by cond(K) eps32,
+        # so the two residuals differ by ~1e-5 absolute (0.5 % after one cycle, 3 % after three, where r has
+        # come down to ~1e-4, measured); a wrong schedule changes the per-cycle contraction (~0.2) far more
+        np.testing.assert_allclose(s3.residual_norm().cpu().numpy(), orc.interior_norm(fb - mg.levels[0].K(v)),
+                                   rtol=1e-2, atol=1e-3 * float(r0.max()), err_msg=f"cycle {k + 1}")

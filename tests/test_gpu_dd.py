@@ -123,3 +123,134 @@ def test_dd_processes_gloo(tmp_path, m, n, P, Ld, grid):
     assert np.array_equal(got, exp), np.nanmax(np.abs(got - exp))
     for r in range(P):
         np.testing.assert_allclose(np.load(os.path.join(tmp_path, f"n{r}.npy")), ref[-1][1].cpu().numpy(), rtol=1e-12)
+
+
+class _FakeDist:
+    """An in-process stand-in for torch.distributed with the nccl backend's behaviour as TorchComm sees it
+    (device buffers sent directly; P2P messages matched per peer pair in posting order; collectives), for
+    ranks running as threads of one process.  A send snapshots its buffer on the stream at posting time."""
+
+    def __init__(self, world):
+        import threading
+        from collections import defaultdict
+        self.world = world
+        self.cv = threading.Condition()
+        self.mail = {}
+        self.nsend = defaultdict(int)
+        self.nrecv = defaultdict(int)
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+        self.tls = threading.local()
+        self.isend, self.irecv = "isend", "irecv"
+        self.posted = []  # (src, dst, numel) in posting order, for the test's own checks
+
+        class P2POp:
+            def __init__(op, kind, tensor, peer, group=None):
+                op.kind, op.tensor, op.peer = kind, tensor, peer
+        self.P2POp = P2POp
+
+    def get_rank(self, group=None):
+        return self.tls.rank
+
+    def get_world_size(self, group=None):
+        return self.world
+
+    def get_backend(self, group=None):
+        return "nccl"
+
+    def batch_isend_irecv(self, ops):
+        me = self.tls.rank
+        works = []
+        with self.cv:
+            for op in ops:
+                if op.kind == "isend":
+                    k = (me, op.peer)
+                    self.mail[k + (self.nsend[k],)] = op.tensor.clone()
+                    self.posted.append((me, op.peer, op.tensor.numel()))
+                    self.nsend[k] += 1
+            self.cv.notify_all()
+        fake = self
+
+        class Work:
+            def __init__(w, key, t):
+                w.key, w.t = key, t
+
+            def wait(w):
+                if w.key is None:
+                    return
+                with fake.cv:
+                    fake.cv.wait_for(lambda: w.key in fake.mail, timeout=60)
+                    src = fake.mail.pop(w.key)
+                assert src.shape == w.t.shape or src.numel() == w.t.numel(), (src.shape, w.t.shape)
+                w.t.copy_(src.reshape(w.t.shape))
+                w.key = None
+        for op in ops:
+            if op.kind == "irecv":
+                k = (op.peer, me)
+                works.append(Work(k + (self.nrecv[k],), op.tensor))
+                self.nrecv[k] += 1
+        return works
+
+    def _gather(self, t):
+        me = self.tls.rank
+        self.slots[me] = t.clone()
+        self.bar.wait()
+        parts = list(self.slots)
+        self.bar.wait()
+        return parts
+
+    def all_gather_into_tensor(self, out, inp, group=None):
+        out.copy_(torch.cat([p.reshape(-1) for p in self._gather(inp)]))
+
+    def all_gather(self, parts, src, group=None):
+        for d, s in zip(parts, self._gather(src)):
+            d.copy_(s)
+
+    def all_reduce(self, t, group=None, op=None):
+        t.copy_(sum(self._gather(t)))
+
+
+@pytest.mark.parametrize("m,n,P,Ld,grid", [(512, 256, 2, 2, (2, 1)), (512, 512, 4, 2, (2, 2)), (512, 1024, 8, 2, (4, 2))])
+def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid):
+    """TorchComm's RCCL branch (device views sent directly when contiguous, packed device strips otherwise,
+    the x phase finished before the y phase, the deferred level-0 exchange, all_gather_into_tensor into the
+    coarse f, all_reduce of the norm) with the ranks as threads over an in-process fake of the nccl
+    backend: bitwise the single-GPU V-cycle.  This is the path the multi-GPU bench takes; one GPU cannot
+    host two RCCL ranks."""
+    import threading
+    from feanet_amd.dd import DDSolver, TorchComm
+    f, u0, bc = _global_problem(m, n, 1, seed=3)
+    _, ref = _single(m, n, 1, f, u0, bc, 3)
+    torch.cuda.synchronize()
+    fake = _FakeDist(P)
+    out, errs = {}, []
+
+    def run(r):
+        try:
+            fake.tls.rank = r
+            comm = TorchComm(dist=fake)
+            assert comm.gpu and comm.rank == r
+            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=False)
+            s.set_rhs(f)
+            s.load(u0, bc)
+            s.vcycle(1)
+            s.vcycle(2)  # joined cycles: the deferred level-0 halo finish
+            out[r] = (s.owned_block(), s.residual_norm())
+        except Exception as e:  # noqa: BLE001
+            errs.append((r, e))
+            fake.bar.abort()
+    th = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    got = torch.full_like(ref[-1][0], float("nan"))
+    for r, (((y0, y1), (x0, x1), u), nr) in out.items():
+        got[:, :, y0:y1, x0:x1] = u
+        torch.testing.assert_close(nr, ref[-1][1], rtol=1e-12, atol=0)
+    assert torch.equal(got, ref[-1][0])
+    # every rank talked to its neighbours only, and both phases ran (rows and, for Pc > 1, columns)
+    assert fake.posted and all(a != b for a, b, _ in fake.posted)
+    assert not fake.mail, "unmatched messages"

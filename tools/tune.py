@@ -1,3 +1,4 @@
+# (historical record: its FEANET_TARGET_WAVES / FEANET_JOIN_RB knobs were removed in round 3; the values it chose are compile-time constants now)
 """Interleaved A/B timing of V-cycle variants in one process (guide §5.4 rule 24).
 
 Each variant = solver kwargs + environment knobs (FEANET_TARGET_WAVES, FEANET_NT_BYTES) that are
