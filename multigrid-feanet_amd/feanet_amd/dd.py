@@ -606,12 +606,15 @@ class DDSolver:
         return self._gstage
 
     def gather_place(self, blocks):
-        """2-D blocks: copy the gathered blocks ([P, B, c_r, c_c], rank order) into the coarse f."""
+        """2-D blocks: copy the gathered blocks ([P, B, c_r, c_c], rank order) into the coarse f — ONE copy
+        between two strided views ([B, Pr, c_r, Pc, c_c] of the staging buffer and of the framed field)."""
         Lc = self.coarse.levels[0]
         c, cc = self.part.rows_per_rank(self.Ld), self.part.cols_per_rank(self.Ld)
-        for q in range(self.P):
-            qi, qj = divmod(q, self.Pc)
-            _block(Lc.f, Lc.B, Lc.bs, Lc.ld, 1 + qi * c, 1 + (qi + 1) * c, 1 + qj * cc, 1 + (qj + 1) * cc).copy_(blocks[q])
+        Pr, Pc, B = self.Pr, self.Pc, Lc.B
+        off = 128 // Lc.f.element_size() - 1
+        dst = Lc.f.as_strided((B, Pr, c, Pc, cc), (Lc.bs, c * Lc.ld, Lc.ld, cc, 1),
+                              Lc.f.storage_offset() + 2 * Lc.ld + off + 1)
+        dst.copy_(blocks.view(Pr, Pc, B, c, cc).permute(2, 0, 3, 1, 4))
 
     def gather(self):
         """The level-Ld all-gather over the communicator (the coarse solver's f on every rank)."""

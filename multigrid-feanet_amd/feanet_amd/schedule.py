@@ -46,9 +46,10 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
     restriction (sweep_restrict).
     top_zero: level 0 starts from a zero guess like the coarse levels (the coarse sub-cycle of a
     domain-decomposed V-cycle, run on the agglomerated level; bitwise the single-grid coarse part).
-    recompute: a coarse level (l >= 1) whose only pre-sweep is the zero-guess one keeps no iterate
-    between its restriction and its prolongation: the prolongation recomputes omd*f_l (V(nu1=1,
-    nu2>=1): 16 B per node less traffic in fp64, bitwise the same)."""
+    recompute: a level starting from zero (l >= 1, and level 0 with top_zero) whose only pre-sweep is the
+    zero-guess one keeps no iterate between its restriction and its prolongation: the prolongation
+    recomputes omd*f_l (V(nu1=1, nu2>=1): 16 B per node less traffic in fp64, bitwise the same; the
+    level's two steps can then join the multi-level launches)."""
     if tail_from is not None and not (1 <= tail_from <= L - 1):
         raise ValueError("vcycle_schedule: tail_from must be in [1, L-1]")
     if L < 1 or nu1 < 0 or nu2 < 0:
@@ -76,7 +77,7 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
             steps.append(("resid_restrict", l, cur[l], None))
             return
         if from_zero and nsweeps == 1:
-            if recompute and l >= 1 and nu2 >= 1:
+            if recompute and (l >= 1 or top_zero) and nu2 >= 1:
                 steps.append(("resid_restrict", l, None, None))
                 cur[l] = OMDF
             else:

@@ -100,6 +100,16 @@ def test_default_agglomeration():
     Partition(16384, 8192, 8, Ld)
 
 
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_c4_agglomeration_level_is_the_measured_best(P):
+    """C4 (8193^2 over the bench's 2x1 / 2x2 / 4x2 blocks): the default agglomeration level is the one the
+    per-rank projection measured fastest — Ld = 4 (the 513^2 level) at every rank count, against Ld = 3, 5, 6
+    (tools/dd_projection.py, profiles/r03_dd/dd_projection.txt: 8 ranks 151.8 us vs 158.5 / 155.9 / 154.7)."""
+    from feanet_amd.dd import default_grid
+    Pr, Pc = default_grid(P)
+    assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == 4
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -213,3 +213,25 @@ def test_mid_grouping_equals_per_level(problem, groups):
     np.testing.assert_array_equal(out, ref)
     assert end == "a" or end == "b"
     np.testing.assert_allclose(out, mg.step(v, f), rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("nu", [(1, 1), (2, 1), (1, 2), (0, 2)])
+def test_top_zero_schedule_equals_step_from_zero(problem, nu):
+    """top_zero (the replicated coarse sub-cycle of the domain-decomposed path): level 0 starts from a zero
+    guess; with one pre-sweep its iterate is not kept but recomputed (omd f) by the prolongation, like the
+    coarse levels', so the whole sub-cycle can run as multi-level launches — the result is the ordinary
+    schedule's from u = 0."""
+    n, L = 32, 5
+    rng = np.random.default_rng(3)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    mg.nu, mg.q2 = nu, False
+    f = rng.standard_normal((2, n + 1, n + 1))
+    ref_steps, ref_end = vcycle_schedule(L, *nu)
+    ref = interpret(mg, ref_steps, np.zeros_like(f), f)[0][ref_end]
+    for tail in (None, 2):
+        steps, end = vcycle_schedule(L, *nu, top_zero=True, tail_from=tail)
+        if nu == (1, 1):
+            assert steps[0] == ("resid_restrict", 0, None, None) and steps[-1][2] == "omdf"
+        out = interpret(mg, steps, rng.standard_normal(f.shape), f)[0][end]
+        np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
