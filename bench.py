@@ -131,6 +131,9 @@ def time_fine_kernels(s, reps):
     name, args = s._join_call("a", L1.a.data_ptr())
     out["fea_mg_cycle_join"] = (time_kernel(name, s.dtype, args, reps, st),
                                 (3 * es + pb) * nodes + (2 * es + pb) * cnodes)
+    if s.smoother == "hjac":  # the learned smoother's fused sweep (Jacobi + 3 masked convs, one pass)
+        args = (L0.a.data_ptr(), None, L0.f.data_ptr(), L0.b.data_ptr(), p0, kt, om, nt, s.hw.data_ptr(), s.nl) + geom
+        out["fea_mg_hsweep"] = (time_kernel("mg_hsweep", s.dtype, args, reps, st), (3 * es + pb) * nodes)
     return out
 
 
@@ -175,13 +178,20 @@ def time_join_in_cycle(s, k):
 
 
 def load_traffic(kernel_key):
+    """Measured HBM bytes per launch from a rocprofv3 PMC record (profiles/pmc_traffic.json), only if it was
+    taken on the kernel source this run executes (SHA-256 stamp of csrc/framed_ops.hip); else (None, why)."""
+    from tools.pmc_traffic import kernel_source_sha
     p = os.environ.get("FEANET_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     if not os.path.exists(p):
         return None, None
     try:
         d = json.load(open(p))
         rec = d.get(kernel_key)
-        return (rec["hbm_bytes_per_launch"], rec.get("source")) if rec else (None, None)
+        if not rec:
+            return None, None
+        if rec.get("kernel_source_sha256") != kernel_source_sha():
+            return None, f"{os.path.relpath(p, ROOT)} was measured on other kernel source (stale), not reported"
+        return rec["hbm_bytes_per_launch"], rec.get("source")
     except Exception:
         return None, None
 
@@ -286,6 +296,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--problem", default="poisson", choices=["poisson", "interface"])
+    ap.add_argument("--levels", type=int, default=None, help="V-cycle levels (default int(log2 n))")
+    ap.add_argument("--smoother", default="jac", choices=["jac", "hjac"],
+                    help="hjac: the learned smoother of M-FEANet-mg_test.ipynb (HRelax, HNet weights "
+                         "feanet_amd/weights/hnet_iso_poisson_33x33.npz), MultiGrid(mode='hjac').Step")
     ap.add_argument("--mode", default=None, choices=["single", "dd", "replicas"],
                     help="default: single at 1 GPU, dd (domain decomposition, weak scaling) at N > 1")
     ap.add_argument("--agglomerate", type=int, default=None, help="dd: level gathered for the coarse solve")
@@ -339,7 +353,12 @@ def main():
                        f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
     else:
         N = n + 1
-        s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B)
+        hnet = None
+        if args.smoother == "hjac":
+            w = np.load(os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
+            hnet = np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+        s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B, levels=args.levels, smoother=args.smoother,
+                            hnet=hnet)
         g.manual_seed(1234 + rank)
         if rhs == "families":
             from tools import rhs_families
@@ -348,8 +367,8 @@ def main():
             s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
         dof = B * N * N * ws
         lvl = s
-        workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics), "
-                    f"batch {B} per GPU")
+        workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics"
+                    f"{', learned HRelax smoother' if args.smoother == 'hjac' else ''}), batch {B} per GPU")
         parallelism = "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"
     s.load()
     # contraction factor over the first 8 cycles (before the fp64 floor), then restart from zero

@@ -9,9 +9,20 @@ WRITE_SIZE is exact for 16 B/lane streaming stores.  Every load/store of the fra
 usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [SUMMARY_TXT]
 """
 import csv
+import hashlib
 import json
+import os
 import sys
 from collections import defaultdict
+
+KERNEL_SOURCE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multigrid-feanet_amd", "csrc",
+                             "framed_ops.hip")
+
+
+def kernel_source_sha():
+    """First 16 hex digits of the SHA-256 of the level kernels' source: bench.py reports stored PMC traffic
+    only for the kernels it was measured on."""
+    return hashlib.sha256(open(KERNEL_SOURCE, "rb").read()).hexdigest()[:16]
 
 
 def load(path, counter):
@@ -50,7 +61,8 @@ def main(fcsv, wcsv, out_json, summary=None, src="profiles/r01_pmc"):
                 "hbm_bytes_per_launch": f + w, "read_bytes_per_launch": f, "write_bytes_per_launch": w,
                 "algorithmic_bytes_per_launch": alg, "launches": n, "grid": grid,
                 "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads), KiB -> bytes",
-                "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({src})"}
+                "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({src})",
+                "kernel_source_sha256": kernel_source_sha()}
     json.dump(res, open(out_json, "w"), indent=1)
     if summary:
         with open(summary, "w") as fh:
