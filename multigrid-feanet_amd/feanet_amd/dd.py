@@ -26,10 +26,11 @@ only where that depth would run out.  Per V-cycle:
                                                        iterate, joined cycles)
   at level Ld:  all-gather of the owned blocks of f_Ld -> the replicated coarse solve -> local copy
   after the finest post-smoothing (unjoined cycles):   D0 of the finest iterate
-An exchange of depth d runs in two phases: x (left/right neighbours: d ghost COLUMNS of the owned rows,
-packed strips) then y (up/down neighbours: d ghost ROWS over the whole local width, contiguous runs of
-the framed layout that now include the ghost columns just received), so the corner regions the
-9-point stencil needs arrive from the diagonal neighbours without corner messages.  D0 and D1 are the
+An exchange of depth d is ONE round of messages with up to eight neighbours (DDSolver.regions): d ghost
+rows of the owned columns from the neighbours above / below, d ghost columns of the owned rows from the
+left / right, and the d x d corner regions the 9-point stencil needs from the diagonal neighbours; all
+regions of one exchange are packed into one staging buffer by one kernel (fea_dd_copy_blocks), sent as one
+message per neighbour and unpacked by one kernel (row slabs: contiguous rows, sent in place).  D0 and D1 are the
 smallest depths for which the validity simulation keeps every owned node exact.
 """
 import torch
@@ -331,13 +332,22 @@ def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None):
 
 
 def _launch_list(launches, dtype, stream):
-    """C-ABI calls and ("copy", (dst, src)) device copies, in order, on `stream`."""
+    """C-ABI calls, ("copy", (dst, src)) device copies and ("fn", f) device steps f(stream), in order, on
+    `stream`."""
     for name, args in launches:
         if name == "copy":
             with torch.cuda.stream(stream):
                 args[0].copy_(args[1])
+        elif name == "fn":  # a communicator's device step (halo pack), launched on `stream`
+            args(stream)
         else:
             _lib.call(name, dtype, *args, stream.cuda_stream)
+
+
+def _split_exchanges(items):
+    """An exchange batch's coarse-level items (needed by the next kernel) and its finest-level items (not
+    waited for until a level-0 kernel runs), in batch order."""
+    return [it for it in items if it[0] != 0], [it for it in items if it[0] == 0]
 
 
 def _rows(t, B, bs, ld, y0, y1):
@@ -474,6 +484,8 @@ class DDSolver:
         the level-0 halo exchange completes only before them (vcycle) — behind the coarse-level
         segments and the all-gather in front of them."""
         segs = []
+        fold = self.comm is not None and hasattr(self.comm, "halo_pack")
+        place = None  # the gathered blocks' placement, folded into the next kernel segment
         for st in steps:
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
                 if self.P == 1:
@@ -484,7 +496,15 @@ class DDSolver:
                     segs.append(("c", ("exchanges", [st[1:]]), False))
                 continue
             if st[0] == "gather" and self.P > 1:
-                segs.append(("c", st, False))
+                if fold and self.Pc > 1 and segs and segs[-1][0] == "k":
+                    # 2-D blocks: the owned block's staging copy ends the kernel segment before the
+                    # all-gather and the placement starts the one after it (captured, not eager launches)
+                    tgt = self.gather_target()
+                    segs[-1][1].append(("copy", (self._gsend, self.gather_source())))
+                    place = ("copy", self.gather_place_views(tgt))
+                    segs.append(("c", ("gather", True), False))
+                else:
+                    segs.append(("c", st, False))
                 continue
             lvl0 = st[0] == "join" or (st[0] not in ("gather", "scatter", "coarse") and st[1] == 0)
             if st[0] == "gather":  # one rank: the all-gather is a device copy
@@ -497,12 +517,24 @@ class DDSolver:
                 launches = [self.local._join_call(st[1], self.local._ptr(1, st[2]))]
             else:
                 launches = [self.local.bind_step(st)]
+            if place is not None:
+                launches, place = [place] + launches, None
             if segs and segs[-1][0] == "k":
                 segs[-1][1].extend(launches)
                 if lvl0:
                     segs[-1] = ("k", segs[-1][1], True)
             else:
                 segs.append(("k", launches, lvl0))
+        if fold:
+            # each exchange batch's pack (TorchComm.halo_pack: one kernel) ends the kernel segment before it
+            for i, (kind, st, _) in enumerate(segs):
+                if kind == "c" and st[0] == "exchanges" and i > 0 and segs[i - 1][0] == "k":
+                    now, later = _split_exchanges(st[1])
+                    for items in (now, later):
+                        f = self.comm.halo_pack(self, items) if items else None
+                        if f is not None:
+                            segs[i - 1][1].append(("fn", f))
+                    segs[i] = ("c", ("exchanges", st[1], True), False)
         return segs
 
     def joinable(self):
@@ -605,26 +637,34 @@ class DDSolver:
             self._gsend = torch.empty((self.B, c, cc), dtype=self.dtype, device=self.device)
         return self._gstage
 
-    def gather_place(self, blocks):
-        """2-D blocks: copy the gathered blocks ([P, B, c_r, c_c], rank order) into the coarse f — ONE copy
-        between two strided views ([B, Pr, c_r, Pc, c_c] of the staging buffer and of the framed field)."""
+    def gather_place_views(self, blocks):
+        """(destination, source) of the placement of the gathered blocks ([P, B, c_r, c_c], rank order) into
+        the coarse f: two strided [B, Pr, c_r, Pc, c_c] views, of the framed field and of the staging buffer."""
         Lc = self.coarse.levels[0]
         c, cc = self.part.rows_per_rank(self.Ld), self.part.cols_per_rank(self.Ld)
         Pr, Pc, B = self.Pr, self.Pc, Lc.B
         off = 128 // Lc.f.element_size() - 1
         dst = Lc.f.as_strided((B, Pr, c, Pc, cc), (Lc.bs, c * Lc.ld, Lc.ld, cc, 1),
                               Lc.f.storage_offset() + 2 * Lc.ld + off + 1)
-        dst.copy_(blocks.view(Pr, Pc, B, c, cc).permute(2, 0, 3, 1, 4))
+        return dst, blocks.view(Pr, Pc, B, c, cc).permute(2, 0, 3, 1, 4)
 
-    def gather(self):
-        """The level-Ld all-gather over the communicator (the coarse solver's f on every rank)."""
+    def gather_place(self, blocks):
+        """2-D blocks: copy the gathered blocks into the coarse f — ONE copy between two strided views."""
+        dst, src = self.gather_place_views(blocks)
+        dst.copy_(src)
+
+    def gather(self, folded=False):
+        """The level-Ld all-gather over the communicator (the coarse solver's f on every rank).  folded: the
+        staging copy and the placement run inside the kernel segments around it (_segs_of)."""
         if self.Pc == 1:
             self.comm.allgather(self.gather_target(), self.gather_source())
             return
         tgt = self.gather_target()
-        self._gsend.copy_(self.gather_source())
+        if not folded:
+            self._gsend.copy_(self.gather_source())
         self.comm.allgather(tgt, self._gsend)
-        self.gather_place(tgt)
+        if not folded:
+            self.gather_place(tgt)
 
     def scatter_views(self, dst):
         """(destination, source): this rank's stored block of the coarse solution -> level Ld's `dst`."""
@@ -641,27 +681,29 @@ class DDSolver:
         d, s = self.scatter_views(dst)
         d.copy_(s)
 
-    def halo(self, l, name, d, phase):
-        """Halo transfers of one exchange phase on level l's buffer `name`, depth d:
-        [(send view, peer rank, receive view)].  x: d ghost columns of the owned rows to/from the left
-        and right neighbours; y: d ghost rows over the whole local width (ghost columns included) to/from
-        the neighbours above and below."""
+    def regions(self, l, name, d):
+        """The halo of depth d on level l's buffer `name`, ONE phase: [(peer, (dy, dx), send view, receive
+        view)] for every neighbour, diagonal ones included — up/down: d rows of the owned columns; left/right:
+        the owned rows of d columns; corners: d x d.  Every send view lies in the sender's OWNED nodes, so all
+        messages can be in flight at once (the two-phase x-then-y form carried the corners through the ghost
+        columns instead, two dependent message rounds).  Row slabs (Pc = 1): whole framed rows (contiguous
+        runs, sent in place)."""
         lp, lq = self.parts[l], self.cparts[l]
         out = []
-        if phase == "x":
-            if self.ci > 0:
-                out.append((self.level_block(l, name, lp.lo, lp.hi, lq.lo, lq.lo + d), self.rank - 1,
-                            self.level_block(l, name, lp.lo, lp.hi, lq.lo - d, lq.lo)))
-            if self.ci < self.Pc - 1:
-                out.append((self.level_block(l, name, lp.lo, lp.hi, lq.hi - d, lq.hi), self.rank + 1,
-                            self.level_block(l, name, lp.lo, lp.hi, lq.hi, lq.hi + d)))
-        else:
-            if self.ri > 0:
-                out.append((self.level_rows(l, name, lp.lo, lp.lo + d), self.rank - self.Pc,
-                            self.level_rows(l, name, lp.lo - d, lp.lo)))
-            if self.ri < self.Pr - 1:
-                out.append((self.level_rows(l, name, lp.hi - d, lp.hi), self.rank + self.Pc,
-                            self.level_rows(l, name, lp.hi, lp.hi + d)))
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                ri, ci = self.ri + dy, self.ci + dx
+                if (dy, dx) == (0, 0) or not (0 <= ri < self.Pr and 0 <= ci < self.Pc):
+                    continue
+                sr, rr = {-1: ((lp.lo, lp.lo + d), (lp.lo - d, lp.lo)), 0: ((lp.lo, lp.hi), (lp.lo, lp.hi)),
+                          1: ((lp.hi - d, lp.hi), (lp.hi, lp.hi + d))}[dy]
+                sc, rc = {-1: ((lq.lo, lq.lo + d), (lq.lo - d, lq.lo)), 0: ((lq.lo, lq.hi), (lq.lo, lq.hi)),
+                          1: ((lq.hi - d, lq.hi), (lq.hi, lq.hi + d))}[dx]
+                if self.Pc == 1:
+                    send, recv = self.level_rows(l, name, *sr), self.level_rows(l, name, *rr)
+                else:
+                    send, recv = self.level_block(l, name, *sr, *sc), self.level_block(l, name, *rr, *rc)
+                out.append((ri * self.Pc + ci, (dy, dx), send, recv))
         return out
 
     # ------------------------------------------------------------------ driver (one process per rank)
@@ -683,17 +725,17 @@ class DDSolver:
                     # halo after, not waited for until a level-0 kernel runs: on RCCL both go out on
                     # the communicator's stream in this order, so the compute stream only waits for
                     # the first batch and level 1 .. Ld-1 run while the finest rows are in flight
-                    now = [it for it in st[1] if it[0] != 0]
-                    later = [it for it in st[1] if it[0] == 0]
+                    now, later = _split_exchanges(st[1])
+                    packed = len(st) > 2 and st[2]
                     if pending is not None:
                         self.comm.exchange_finish(pending)
                         pending = None
                     if now:
-                        self.comm.exchange_many(self, now)
+                        self.comm.exchange_many(self, now, packed=packed)
                     if later:
-                        pending = self.comm.exchange_many(self, later, wait=False)
+                        pending = self.comm.exchange_many(self, later, wait=False, packed=packed)
                 elif st[0] == "gather":
-                    self.gather()
+                    self.gather(folded=len(st) > 1 and st[1] is True)
                 elif st[0] == "scatter":
                     self.scatter(st[1])
         if pending is not None:
@@ -716,6 +758,63 @@ def _boundary_mask(H, W, like):
     return m
 
 
+_DD_BLOCK_WORDS = 4  # fea_dd_copy_blocks record: int64 base, int64 stage, int64 ld, int32 rows + int32 cols
+
+
+class _Staging:
+    """Pack / unpack of a list of [B, rows, cols] (or [B, run]) framed-buffer views to / from one contiguous staging buffer
+    (fea_dd_copy_blocks: one launch for all of them).  Views are concatenated in order."""
+
+    def __init__(self, views, device, dtype):
+        import numpy as np
+        recs, off, mx = [], 0, 1
+        self.offsets = []
+        for v in views:
+            if v.dim() == 2:  # [B, run]: whole framed rows of a row slab
+                (B, cols), (bs, one), rows, ld = v.shape, v.stride(), 1, v.shape[1]
+            else:
+                (B, rows, cols), (bs, ld, one) = v.shape, v.stride()
+            assert one == 1
+            self.offsets.append(off)
+            for b in range(B):
+                recs.append((v.data_ptr() + b * bs * v.element_size(), off, ld, rows | (cols << 32)))
+                off += rows * cols
+            mx = max(mx, rows * cols)
+        self.n = off
+        self.nblocks = len(recs)
+        self.max_elems = mx
+        self.esz = views[0].element_size()
+        if not 0 < self.nblocks <= 65535:
+            raise ValueError(f"feanet_amd.dd: {self.nblocks} staged blocks (1 .. 65535 per launch)")
+        self.desc = torch.from_numpy(np.array(recs, dtype=np.int64).reshape(-1)).to(device)
+        self.buf = torch.empty(max(off, 1), dtype=dtype, device=device)
+
+    def copy(self, to_stage, stream=None):
+        stream = torch.cuda.current_stream(self.buf.device) if stream is None else stream
+        _lib.call_raw("dd_copy_blocks", self.desc.data_ptr(), self.nblocks, self.max_elems, self.buf.data_ptr(),
+                      self.esz, int(to_stage), stream.cuda_stream)
+
+
+def halo_staging(regs):
+    """Staging of one exchange's regions (DDSolver.regions of all its items): the send views grouped per
+    neighbour (in item order, the order the neighbour unpacks them in) in one buffer, the receive views
+    likewise in another; seg_s / seg_r: (peer, element offset, element count) of each neighbour's message."""
+    peers = sorted({p for p, _, _, _ in regs})
+    by_send = [[a for p, _, a, _ in regs if p == q] for q in peers]
+    by_recv = [[b for p, _, _, b in regs if p == q] for q in peers]
+    dev, dt = regs[0][2].device, regs[0][2].dtype
+    send = _Staging([v for vs in by_send for v in vs], dev, dt)
+    recv = _Staging([v for vs in by_recv for v in vs], dev, dt)
+    seg_s, seg_r, i_s, i_r = [], [], 0, 0
+    for q, vs, vr in zip(peers, by_send, by_recv):
+        ns, nr = sum(v.numel() for v in vs), sum(v.numel() for v in vr)
+        seg_s.append((q, i_s, ns))
+        seg_r.append((q, i_r, nr))
+        i_s += ns
+        i_r += nr
+    return send, recv, seg_s, seg_r
+
+
 class TorchComm:
     """Halo exchange / all-gather / all-reduce over torch.distributed.  With the nccl backend (RCCL
     on ROCm) device buffers are sent directly; with gloo they are staged through host memory."""
@@ -729,74 +828,91 @@ class TorchComm:
         self.world = dist.get_world_size(group)
         self.gpu = dist.get_backend(group) == "nccl"
 
-    def _stage(self, t):
-        return t.contiguous() if self.gpu else t.cpu()
-
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])
 
-    def _phase_plan(self, s, items, phase):
-        """P2P ops of one exchange phase for every (level, buffer, d) in `items` (DDSolver.halo), with
-        send/receive buffers: the views themselves when they are contiguous device rows (RCCL), else
-        staging buffers (packed column strips; host memory for gloo)."""
+    def _plan(self, s, items):
+        """One round of P2P messages for every (level, buffer, depth) in `items` (DDSolver.regions, diagonal
+        neighbours included).  Row slabs with RCCL: each region is a contiguous run of the framed layout and
+        is sent / received in place.  Otherwise: every region of all items is packed into one staging buffer
+        with one kernel, ONE message per neighbour (its regions in item order — the peer unpacks in the same
+        order), and unpacked with one kernel; gloo moves the staging buffers through host memory."""
         dist = self.dist
-        trans = [t for l, name, d in items for t in s.halo(l, name, d, phase)]
-        direct = self.gpu and all(a.is_contiguous() and b.is_contiguous() for a, _, b in trans)
+        regs = [r for l, name, d in items for r in s.regions(l, name, d)]
+        if not regs:
+            return {"ops": [], "direct": True}
+        direct = self.gpu and all(a.is_contiguous() and b.is_contiguous() for _, _, a, b in regs)
         if direct:
-            sb = [a for a, _, _ in trans]
-            rb = [b for _, _, b in trans]
+            ops = [dist.P2POp(dist.isend, a, p, self.group) for p, _, a, _ in regs]
+            ops += [dist.P2POp(dist.irecv, b, p, self.group) for p, _, _, b in regs]
+            return {"ops": ops, "direct": True}
+        send, recv, seg_s, seg_r = halo_staging(regs)
+        dt = send.buf.dtype
+        if self.gpu:
+            sb, rb = send.buf, recv.buf
         else:
-            dev = trans[0][0].device if (trans and self.gpu) else "cpu"
-            sb = [torch.empty(a.shape, dtype=a.dtype, device=dev) for a, _, _ in trans]
-            rb = [torch.empty(b.shape, dtype=b.dtype, device=dev) for _, _, b in trans]
-        ops = [dist.P2POp(dist.isend, b, peer, self.group) for b, (_, peer, _) in zip(sb, trans)]
-        ops += [dist.P2POp(dist.irecv, b, peer, self.group) for b, (_, peer, _) in zip(rb, trans)]
-        return (ops, direct, list(zip(sb, [a for a, _, _ in trans])), list(zip(rb, [b for _, _, b in trans])))
+            sb, rb = torch.empty(send.buf.shape, dtype=dt), torch.empty(recv.buf.shape, dtype=dt)
+        ops = [dist.P2POp(dist.isend, sb[o:o + n], q, self.group) for q, o, n in seg_s]
+        ops += [dist.P2POp(dist.irecv, rb[o:o + n], q, self.group) for q, o, n in seg_r]
+        return {"ops": ops, "direct": False, "send": send, "recv": recv, "sb": sb, "rb": rb}
 
-    def exchange_many(self, s, items, wait=True):
-        """Refresh d ghost lines around rank s's block for every (level, buffer, d) in `items`: the x phase
-        (ghost columns, left/right neighbours) as ONE batch of P2P ops, completed, then the y phase (ghost
-        rows incl. the new ghost columns, up/down) as one batch.  The op lists are built once per item
-        list and reused (fixed device views).  wait=False: return a handle for exchange_finish instead
-        of completing the last batch (with RCCL its ops run on the communicator's stream meanwhile;
-        finishing makes the current stream wait for them, the host does not block)."""
-        dist = self.dist
+    def _cached_plan(self, s, items):
         # plans hold views of s's buffers: cached on s itself (keyed by this communicator), never on
         # the communicator under id(s), which a later solver could reuse
         plans = s.__dict__.setdefault("_comm_plans", {})
         key = (id(self), tuple(items))
-        phases = plans.get(key)
-        if phases is None:
-            phases = [self._phase_plan(s, items, ph) for ph, n in (("x", s.Pc), ("y", s.Pr)) if n > 1]
-            phases = [p for p in phases if p[0]]
-            plans[key] = phases
-        handle = None
-        for i, (ops, direct, spairs, rpairs) in enumerate(phases):
-            if not direct:
-                for b, t in spairs:
-                    b.copy_(t)
-            handle = (dist.batch_isend_irecv(ops), direct, rpairs)
-            if wait or i < len(phases) - 1:
-                self.exchange_finish(handle)
-                handle = None
+        plan = plans.get(key)
+        if plan is None:
+            plan = self._plan(s, items)
+            plans[key] = plan
+        return plan
+
+    def halo_pack(self, s, items):
+        """The device step that packs the send regions of exchange_many(s, items) — f(stream) — or None when
+        the regions go out in place.  The solver launches it inside its kernel segment (captured in the
+        segment's graph) and then calls exchange_many(..., packed=True)."""
+        plan = self._cached_plan(s, items)
+        if not plan["ops"] or plan["direct"]:
+            return None
+        return lambda stream: plan["send"].copy(True, stream)
+
+    def exchange_many(self, s, items, wait=True, packed=False):
+        """Refresh d ghost lines around rank s's block for every (level, buffer, d) in `items`: pack, ONE
+        batch of P2P ops with every neighbour (diagonal ones included), unpack.  The plans are built once per
+        item list and reused (fixed device views).  packed: the pack already ran (halo_pack).  wait=False: return a handle for exchange_finish instead of
+        completing the batch (with RCCL its ops run on the communicator's stream meanwhile; finishing makes
+        the current stream wait for them and unpacks, the host does not block)."""
+        plan = self._cached_plan(s, items)
+        if not plan["ops"]:
+            return None
+        if not plan["direct"]:
+            if not packed:
+                plan["send"].copy(True)
+            if not self.gpu:
+                plan["sb"].copy_(plan["send"].buf)
+        handle = (self.dist.batch_isend_irecv(plan["ops"]), plan)
+        if wait:
+            self.exchange_finish(handle)
+            return None
         return handle
 
     def exchange_finish(self, handle):
         if handle is None:
             return
-        works, direct, rpairs = handle
+        works, plan = handle
         for w in works:
             w.wait()
-        if not direct:
-            for b, t in rpairs:
-                t.copy_(b)
+        if not plan["direct"]:
+            if not self.gpu:
+                plan["recv"].buf.copy_(plan["rb"])
+            plan["recv"].copy(False)
 
     def allgather(self, target, source):
         dist = self.dist
         if self.gpu and target.is_contiguous() and source.is_contiguous():
             dist.all_gather_into_tensor(target.reshape(-1), source.reshape(-1), group=self.group)
             return
-        src = self._stage(source)
+        src = source.contiguous() if self.gpu else source.cpu()
         parts = [torch.empty_like(src) for _ in range(self.world)]
         dist.all_gather(parts, src, group=self.group)
         if target.dim() == 4:  # 2-D blocks: [P, B, c_r, c_c] staging, rank order
@@ -862,15 +978,13 @@ class LocalGroup:
             s._state = end
 
     def _exchange(self, l, name, d):
-        """The two phases of TorchComm.exchange_many as device copies: every rank's x phase, then every
-        rank's y phase (which carries the ghost columns just received)."""
-        for phase in ("x", "y"):
-            for s in self.ranks:
-                for send, peer, _ in s.halo(l, name, d, phase):
-                    q = self.ranks[peer]
-                    # the peer's receive view that pairs with this send (the opposite side)
-                    recv = [rv for _, pr, rv in q.halo(l, name, d, phase) if pr == s.rank]
-                    recv[0].copy_(send)
+        """TorchComm.exchange_many as device copies: every receive region from its peer's matching send
+        region (the one facing the receiver).  Sends read owned nodes only, so the order does not matter."""
+        for q in self.ranks:
+            for peer, (dy, dx), _, recv in q.regions(l, name, d):
+                p = self.ranks[peer]
+                send = [sv for pr, dr, sv, _ in p.regions(l, name, d) if pr == q.rank and dr == (-dy, -dx)]
+                recv.copy_(send[0])
 
     def solution(self):
         """Global iterate assembled from the ranks' owned blocks (they tile the grid)."""

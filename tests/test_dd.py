@@ -127,7 +127,7 @@ def _worker(rank, world, m, n, Ld, port, outdir, grid):
                                            (64, 64, 4, 2, (2, 2)), (64, 128, 2, 2, (1, 2)),
                                            (128, 96, 6, 2, (2, 3))])
 def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld, grid):
-    """Row slabs and 2-D blocks (x-then-y halo exchange, corners via the diagonal neighbours) over gloo,
+    """Row slabs and 2-D blocks (the oracle rank model exchanges x then y: corners via the diagonal neighbours) over gloo,
     world sizes 2..6, against the oracle's single-grid V-cycle on the global grid."""
     import dd_oracle
     mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path), grid), nprocs=P, join=True)

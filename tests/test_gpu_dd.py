@@ -46,7 +46,7 @@ def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1)):
                                                       (4096, 512, 4, 5, 1, True, (1, 1), None),
                                                       (1024, 512, 4, 3, 1, True, (2, 2), None),
                                                       (1024, 512, 2, 3, 1, False, (2, 1), None),
-                                                      # 2-D blocks (x-then-y exchange, corners via diagonals)
+                                                      # 2-D blocks (one-phase exchange, corners from the diagonal neighbours)
                                                       (512, 512, 4, 2, 2, True, (1, 1), (2, 2)),
                                                       (1024, 1024, 8, 3, 1, True, (1, 1), (4, 2)),
                                                       (512, 1024, 2, 3, 1, True, (1, 1), (1, 2)),

@@ -3,7 +3,8 @@
 For a global grid split over P ranks (Pr x Pc blocks), one rank's whole program — its distributed levels
 0 .. Ld-1 with their ghost lines, the agglomeration copies and the redundant coarse sub-cycle (levels >= Ld
 of the global grid) — runs on this GPU with a communicator that moves nothing (NullComm): the time per
-V-cycle is that rank's kernel time, i.e. the N-GPU cycle time without communication.  The rank with the
+V-cycle is that rank's kernel time, i.e. the N-GPU cycle time without communication (PackComm, the default,
+runs the halo pack / unpack kernels of every exchange too; --no-pack leaves them out).  The rank with the
 most ghost lines (an interior block) bounds the cycle.  Reported per Ld beside the single-GPU solver on the
 same global grid, so the agglomeration level can be chosen from measurements.
 
@@ -20,7 +21,7 @@ sys.path.insert(0, os.path.join(HERE, ".."))
 sys.path.insert(0, os.path.join(HERE, "..", "multigrid-feanet_amd"))
 import torch  # noqa: E402
 
-from feanet_amd.dd import DDSolver, default_grid, default_agglomeration, global_levels  # noqa: E402
+from feanet_amd.dd import DDSolver, default_grid, default_agglomeration, global_levels, halo_staging  # noqa: E402
 from feanet_amd.solver import MultigridSolver  # noqa: E402
 
 
@@ -29,7 +30,7 @@ class NullComm:
     identity.  Only for timing one rank's kernels (values are not those of a real decomposition)."""
     gpu = True
 
-    def exchange_many(self, s, items, wait=True):
+    def exchange_many(self, s, items, wait=True, packed=False):
         return None
 
     def exchange(self, s, l, name, d):
@@ -43,6 +44,35 @@ class NullComm:
 
     def allreduce_sum(self, t):
         return t
+
+
+class PackComm(NullComm):
+    """NullComm plus the halo exchange's device work: the pack into the staging buffer (folded into the kernel
+    segment before the exchange, as with TorchComm) and the unpack from it (dd.halo_staging: the same kernels
+    and plans as TorchComm) — only the messages are missing."""
+
+    def _staging(self, s, items):
+        plans = s.__dict__.setdefault("_pack_plans", {})
+        if tuple(items) not in plans:
+            regs = [r for l, name, d in items for r in s.regions(l, name, d)]
+            direct = all(a.is_contiguous() and b.is_contiguous() for _, _, a, b in regs)  # row slabs: in place
+            st = halo_staging(regs)[:2] if regs and not direct else None
+            if st is not None:
+                st[1].buf.zero_()
+            plans[tuple(items)] = st
+        return plans[tuple(items)]
+
+    def halo_pack(self, s, items):
+        st = self._staging(s, items)
+        return None if st is None else (lambda stream: st[0].copy(True, stream))
+
+    def exchange_many(self, s, items, wait=True, packed=False):
+        st = self._staging(s, items)
+        if st is not None:
+            if not packed:
+                st[0].copy(True)
+            st[1].copy(False)
+        return None
 
 
 def time_cycles(vcycle, steps, reps=3):
@@ -73,6 +103,7 @@ def main():
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--ld", default=None, help="agglomeration levels to try (default: default-1 .. default+2)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-pack", action="store_true", help="leave out the halo pack / unpack kernels")
     args = ap.parse_args()
     n = args.n
     g = torch.Generator(device="cuda")
@@ -95,7 +126,7 @@ def main():
         rec["ranks"][P] = {"grid": f"{Pr}x{Pc}", "rank": r, "default_ld": d, "ld": {}}
         for Ld in lds:
             try:
-                s = DDSolver(n, n, r, P, comm=NullComm(), agglomerate=Ld, grid=(Pr, Pc))
+                s = DDSolver(n, n, r, P, comm=NullComm() if args.no_pack else PackComm(), agglomerate=Ld, grid=(Pr, Pc))
             except ValueError as e:
                 print(f"P={P} {Pr}x{Pc} Ld={Ld}: not partitionable ({e})", flush=True)
                 continue
