@@ -22,7 +22,7 @@ Also reported on the same JSON line:
 
 Multi-GPU (torchrun, one process per GPU): domain decomposition (feanet_amd.dd) of ONE global grid,
 8193^2 by default (BASELINE config C4; strong scaling: the same grid over 2, 4, 8 GPUs), 2-D blocks
-(2x1, 2x2, 4x2) with a two-phase RCCL halo exchange once per V-cycle and an agglomerated coarse
+(2x1, 2x2, 4x2) with a one-phase RCCL halo exchange (up to eight neighbours) once per V-cycle and an agglomerated coarse
 solve; value = global DoF / t_step.  --weak keeps 4096 x 4096 intervals per GPU instead (4097^2,
 8193x4097, 8193^2, 16385x8193); --mode replicas runs independent problems.  At N = 1 the default is
 the metric configuration (4097^2, one GPU, no decomposition).  Timing: barrier + synchronize on both
@@ -349,7 +349,7 @@ def main():
                     f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
                     f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
                     + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))
-        parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (x then y phase, depths "
+        parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (one phase, packed, depths "
                        f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
     else:
         N = n + 1

@@ -364,13 +364,12 @@ int fea_mg_mid_up_f64(const double* const* f, const double* e, double* out, cons
 long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi);
 
 /* Domain decomposition (feanet_amd.dd): the halo exchange's pack / unpack in one launch.
- * blocks: device array of nblocks records {int64 base (device address of a block in a framed buffer),
- * int64 stage (element offset in the staging buffer), int64 ld (row pitch, elements), int32 rows,
- * int32 cols}; to_stage = 1 copies every block into stage (row-major, rows x cols), 0 back out of it.
- * max_elems: the largest rows x cols (sizes the grid).  elem_size 4 or 8.  No reference counterpart
- * (the reference is single-process): it packs the messages of the new multi-GPU path. */
-int fea_dd_copy_blocks(const void* blocks, int nblocks, long long max_elems, void* stage, int elem_size,
-                       int to_stage, void* stream);
+ * blocks: HOST array of nblocks records {int64 frame (device address of a block in a framed buffer),
+ * int64 stage (device address of the block in a staging buffer), int64 ld (row pitch, elements), int32 rows,
+ * int32 cols}, copied into the kernel arguments (48 blocks per launch); to_stage = 1 copies every block into
+ * its stage (row-major, rows x cols), 0 back out of it.  elem_size 4 or 8.  No reference counterpart (the
+ * reference is single-process): it packs the messages of the new multi-GPU path. */
+int fea_dd_copy_blocks(const void* blocks, int nblocks, int elem_size, int to_stage, void* stream);
 
 /* On-device mesh set-up: the MeshCenterInterface node pattern map — replaces
  * FEANet/mesh.py place_circle / place_rect (:62-76), identify_patterns (:78-93) and

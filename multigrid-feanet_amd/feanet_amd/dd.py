@@ -344,9 +344,11 @@ def _launch_list(launches, dtype, stream):
             _lib.call(name, dtype, *args, stream.cuda_stream)
 
 
-def _split_exchanges(items):
-    """An exchange batch's coarse-level items (needed by the next kernel) and its finest-level items (not
-    waited for until a level-0 kernel runs), in batch order."""
+def _split_exchanges(items, overlap_l0=False):
+    """An exchange batch as (now, later): later = its finest-level items when overlap_l0 (not waited for until
+    a level-0 kernel runs), else nothing (one message batch and one unpack for all of it)."""
+    if not overlap_l0:
+        return list(items), []
     return [it for it in items if it[0] != 0], [it for it in items if it[0] == 0]
 
 
@@ -367,13 +369,16 @@ class DDSolver:
     Args: n, rows: global intervals (columns, rows) of the fine grid; rank, world: this rank and the
     number of ranks; grid: (Pr, Pc) blocks, Pr * Pc = world (default (world, 1): row slabs; see
     default_grid for the 2-D choice); comm: a TorchComm (one process per GPU) or None when driven by a
-    LocalGroup; agglomerate: Ld (default: see default_agglomeration); other args as MultigridSolver
-    (Poisson).
+    LocalGroup; agglomerate: Ld (default: see default_agglomeration); overlap_l0: send the finest level's halo
+    as a second message batch that completes only before the next level-0 kernel (overlapping levels 1 .. and
+    the coarse solve) instead of with the coarse-level halo in one batch — one more message group and one
+    more unpack launch per cycle; other args as MultigridSolver (Poisson).
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
-                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None):
+                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False):
         self.n, self.m = n, rows
+        self.overlap_l0 = overlap_l0
         self.rank, self.P = rank, world
         self.Pr, self.Pc = grid if grid is not None else (world, 1)
         self.ri, self.ci = divmod(rank, self.Pc)
@@ -529,11 +534,9 @@ class DDSolver:
             # each exchange batch's pack (TorchComm.halo_pack: one kernel) ends the kernel segment before it
             for i, (kind, st, _) in enumerate(segs):
                 if kind == "c" and st[0] == "exchanges" and i > 0 and segs[i - 1][0] == "k":
-                    now, later = _split_exchanges(st[1])
-                    for items in (now, later):
-                        f = self.comm.halo_pack(self, items) if items else None
-                        if f is not None:
-                            segs[i - 1][1].append(("fn", f))
+                    f = self.comm.halo_pack(self, *_split_exchanges(st[1], self.overlap_l0))
+                    if f is not None:
+                        segs[i - 1][1].append(("fn", f))
                     segs[i] = ("c", ("exchanges", st[1], True), False)
         return segs
 
@@ -725,7 +728,7 @@ class DDSolver:
                     # halo after, not waited for until a level-0 kernel runs: on RCCL both go out on
                     # the communicator's stream in this order, so the compute stream only waits for
                     # the first batch and level 1 .. Ld-1 run while the finest rows are in flight
-                    now, later = _split_exchanges(st[1])
+                    now, later = _split_exchanges(st[1], self.overlap_l0)
                     packed = len(st) > 2 and st[2]
                     if pending is not None:
                         self.comm.exchange_finish(pending)
@@ -762,37 +765,41 @@ _DD_BLOCK_WORDS = 4  # fea_dd_copy_blocks record: int64 base, int64 stage, int64
 
 
 class _Staging:
-    """Pack / unpack of a list of [B, rows, cols] (or [B, run]) framed-buffer views to / from one contiguous staging buffer
-    (fea_dd_copy_blocks: one launch for all of them).  Views are concatenated in order."""
+    """Pack / unpack of a list of [B, rows, cols] (or [B, run]) framed-buffer views to / from one contiguous
+    staging buffer (fea_dd_copy_blocks: one launch for all of them).  Views are concatenated in order.
+    `records`: the block table (host int64 [nblocks, 4]); copy_blocks() launches any concatenation of them."""
 
     def __init__(self, views, device, dtype):
         import numpy as np
-        recs, off, mx = [], 0, 1
-        self.offsets = []
+        sizes = []
         for v in views:
             if v.dim() == 2:  # [B, run]: whole framed rows of a row slab
                 (B, cols), (bs, one), rows, ld = v.shape, v.stride(), 1, v.shape[1]
             else:
                 (B, rows, cols), (bs, ld, one) = v.shape, v.stride()
             assert one == 1
-            self.offsets.append(off)
+            sizes.append((B, rows, cols, bs, ld))
+        self.n = sum(B * rows * cols for B, rows, cols, _, _ in sizes)
+        self.buf = torch.empty(max(self.n, 1), dtype=dtype, device=device)
+        self.esz = self.buf.element_size()
+        recs, off = [], 0
+        for v, (B, rows, cols, bs, ld) in zip(views, sizes):
             for b in range(B):
-                recs.append((v.data_ptr() + b * bs * v.element_size(), off, ld, rows | (cols << 32)))
+                recs.append((v.data_ptr() + b * bs * self.esz, self.buf.data_ptr() + off * self.esz, ld,
+                             rows | (cols << 32)))
                 off += rows * cols
-            mx = max(mx, rows * cols)
-        self.n = off
-        self.nblocks = len(recs)
-        self.max_elems = mx
-        self.esz = views[0].element_size()
-        if not 0 < self.nblocks <= 65535:
-            raise ValueError(f"feanet_amd.dd: {self.nblocks} staged blocks (1 .. 65535 per launch)")
-        self.desc = torch.from_numpy(np.array(recs, dtype=np.int64).reshape(-1)).to(device)
-        self.buf = torch.empty(max(off, 1), dtype=dtype, device=device)
+        self.records = np.array(recs, dtype=np.int64).reshape(-1, _DD_BLOCK_WORDS)
 
     def copy(self, to_stage, stream=None):
-        stream = torch.cuda.current_stream(self.buf.device) if stream is None else stream
-        _lib.call_raw("dd_copy_blocks", self.desc.data_ptr(), self.nblocks, self.max_elems, self.buf.data_ptr(),
-                      self.esz, int(to_stage), stream.cuda_stream)
+        copy_blocks(self.records, to_stage, self.esz, self.buf.device, stream)
+
+
+def copy_blocks(records, to_stage, esz, device, stream=None):
+    """One fea_dd_copy_blocks launch (per 48 blocks) over a block table (host int64 [nblocks, 4])."""
+    import numpy as np
+    recs = np.ascontiguousarray(records, dtype=np.int64)
+    stream = torch.cuda.current_stream(device) if stream is None else stream
+    _lib.call_raw("dd_copy_blocks", recs.ctypes.data, len(recs), esz, int(to_stage), stream.cuda_stream)
 
 
 def halo_staging(regs):
@@ -867,14 +874,19 @@ class TorchComm:
             plans[key] = plan
         return plan
 
-    def halo_pack(self, s, items):
-        """The device step that packs the send regions of exchange_many(s, items) — f(stream) — or None when
-        the regions go out in place.  The solver launches it inside its kernel segment (captured in the
-        segment's graph) and then calls exchange_many(..., packed=True)."""
-        plan = self._cached_plan(s, items)
-        if not plan["ops"] or plan["direct"]:
+    def halo_pack(self, s, *item_lists):
+        """The device step that packs the send regions of exchange_many(s, items) for every items in
+        item_lists — ONE launch, f(stream) — or None when all regions go out in place.  The solver launches it
+        inside its kernel segment (captured in the segment's graph) and then calls
+        exchange_many(..., packed=True)."""
+        import numpy as np
+        sends = [p["send"] for p in (self._cached_plan(s, items) for items in item_lists if items)
+                 if p["ops"] and not p["direct"]]
+        if not sends:
             return None
-        return lambda stream: plan["send"].copy(True, stream)
+        recs = np.concatenate([st.records for st in sends])
+        esz, dev = sends[0].esz, sends[0].buf.device
+        return lambda stream: copy_blocks(recs, True, esz, dev, stream)
 
     def exchange_many(self, s, items, wait=True, packed=False):
         """Refresh d ghost lines around rank s's block for every (level, buffer, d) in `items`: pack, ONE

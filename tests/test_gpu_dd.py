@@ -210,13 +210,14 @@ class _FakeDist:
         t.copy_(sum(self._gather(t)))
 
 
+@pytest.mark.parametrize("overlap_l0", [False, True])
 @pytest.mark.parametrize("m,n,P,Ld,grid", [(512, 256, 2, 2, (2, 1)), (512, 512, 4, 2, (2, 2)), (512, 1024, 8, 2, (4, 2))])
-def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid):
-    """TorchComm's RCCL branch (device views sent directly when contiguous, packed device strips otherwise,
-    the x phase finished before the y phase, the deferred level-0 exchange, all_gather_into_tensor into the
-    coarse f, all_reduce of the norm) with the ranks as threads over an in-process fake of the nccl
-    backend: bitwise the single-GPU V-cycle.  This is the path the multi-GPU bench takes; one GPU cannot
-    host two RCCL ranks."""
+def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0):
+    """TorchComm's RCCL branch (device views sent directly when contiguous; otherwise the one-phase packed
+    batch with its pack inside the kernel segment, one message per neighbour including the diagonal ones;
+    with overlap_l0 the deferred level-0 exchange; all_gather_into_tensor into the coarse f, all_reduce of
+    the norm) with the ranks as threads over an in-process fake of the nccl backend: bitwise the
+    single-GPU V-cycle.  This is the path the multi-GPU bench takes; one GPU cannot host two RCCL ranks."""
     import threading
     from feanet_amd.dd import DDSolver, TorchComm
     f, u0, bc = _global_problem(m, n, 1, seed=3)
@@ -230,7 +231,7 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid):
             fake.tls.rank = r
             comm = TorchComm(dist=fake)
             assert comm.gpu and comm.rank == r
-            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=False)
+            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=False, overlap_l0=overlap_l0)
             s.set_rhs(f)
             s.load(u0, bc)
             s.vcycle(1)
@@ -251,6 +252,10 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid):
         got[:, :, y0:y1, x0:x1] = u
         torch.testing.assert_close(nr, ref[-1][1], rtol=1e-12, atol=0)
     assert torch.equal(got, ref[-1][0])
-    # every rank talked to its neighbours only, and both phases ran (rows and, for Pc > 1, columns)
+    # every rank talked to its (up to eight) neighbours only; 2-D grids: the diagonal ones too
     assert fake.posted and all(a != b for a, b, _ in fake.posted)
+    pairs = {(divmod(a, grid[1]), divmod(b, grid[1])) for a, b, _ in fake.posted}
+    assert all(abs(ya - yb) <= 1 and abs(xa - xb) <= 1 for (ya, xa), (yb, xb) in pairs)
+    if grid[1] > 1:
+        assert any(ya != yb and xa != xb for (ya, xa), (yb, xb) in pairs)
     assert not fake.mail, "unmatched messages"

@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(HERE, ".."))
 sys.path.insert(0, os.path.join(HERE, "..", "multigrid-feanet_amd"))
 import torch  # noqa: E402
 
-from feanet_amd.dd import DDSolver, default_grid, default_agglomeration, global_levels, halo_staging  # noqa: E402
+from feanet_amd.dd import DDSolver, default_grid, default_agglomeration, global_levels, halo_staging, copy_blocks  # noqa: E402
 from feanet_amd.solver import MultigridSolver  # noqa: E402
 
 
@@ -62,9 +62,13 @@ class PackComm(NullComm):
             plans[tuple(items)] = st
         return plans[tuple(items)]
 
-    def halo_pack(self, s, items):
-        st = self._staging(s, items)
-        return None if st is None else (lambda stream: st[0].copy(True, stream))
+    def halo_pack(self, s, *item_lists):
+        import numpy as np
+        sends = [st[0] for st in (self._staging(s, items) for items in item_lists if items) if st is not None]
+        if not sends:
+            return None
+        recs = np.concatenate([x.records for x in sends])
+        return lambda stream: copy_blocks(recs, True, sends[0].esz, sends[0].buf.device, stream)
 
     def exchange_many(self, s, items, wait=True, packed=False):
         st = self._staging(s, items)
@@ -83,9 +87,12 @@ def time_cycles(vcycle, steps, reps=3):
     for _ in range(reps):
         t0 = time.perf_counter()
         vcycle(steps)
+        th = (time.perf_counter() - t0) / steps  # host issue time (the GPU is host-bound when it is ~ t)
         torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / steps
-        best = t if best is None else min(best, t)
+        if best is None or t < best:
+            best = t
+            time_cycles.host = th
     return best
 
 
@@ -133,6 +140,7 @@ def main():
             s.set_rhs(f)
             s.load()
             t = time_cycles(s.vcycle, args.steps)
+            th = time_cycles.host
             c = s.coarse
             c.set_rhs(f=torch.randn(1, 1, c.H, c.W, dtype=torch.float64, device="cuda", generator=g))
 
@@ -142,11 +150,11 @@ def main():
                     c._vcycles_plain(1)
             tc = time_cycles(coarse_only, args.steps)
             p0, q0 = s.parts[0], s.cparts[0]
-            info = {"us_per_cycle": t * 1e6, "coarse_subcycle_us": tc * 1e6,
+            info = {"us_per_cycle": t * 1e6, "host_issue_us_per_cycle": th * 1e6, "coarse_subcycle_us": tc * 1e6,
                     "local_fine": f"{p0.Hloc}x{q0.Hloc}", "ghost0": s.part.ghost(0), "depths": list(s.depths),
                     "coarse_grid": f"{c.H}x{c.W}", "projected_speedup": t1 / t}
             rec["ranks"][P]["ld"][Ld] = info
-            print(f"P={P} {Pr}x{Pc} rank {r} Ld={Ld}: {t * 1e6:7.1f} us per cycle (coarse sub-cycle {tc * 1e6:5.1f} "
+            print(f"P={P} {Pr}x{Pc} rank {r} Ld={Ld}: {t * 1e6:7.1f} us per cycle (host issue {th * 1e6:5.1f} us; coarse sub-cycle {tc * 1e6:5.1f} "
                   f"us on {c.H}x{c.W}; local fine {p0.Hloc}x{q0.Hloc}, ghost {s.part.ghost(0)}), speed-up "
                   f"{t1 / t:.2f} (no communication)", flush=True)
             del s, c
