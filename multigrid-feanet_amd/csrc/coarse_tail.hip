@@ -422,7 +422,10 @@ __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, co
   }
 }
 
-template <typename T, bool MULTI>
+// FIX65: the V(1,1) 65^2 / 6-level tail of every BASELINE configuration only — a kernel of its own, so the
+// register allocation is that path's alone (sharing one kernel with the general paths spilled 16 VGPRs of
+// the fp64 single-pattern variant to scratch, reloaded inside the phases).
+template <typename T, bool MULTI, bool FIX65 = false>
 __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kTailLdsBytes];
   const int tid = threadIdx.x;
@@ -442,11 +445,11 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
 
   // V(1,1) (the default MultiGrid.Step / iterate schedule) runs the fused row-wave path below; it
   // masks every read outside a level's interior, so only the general path needs zeroed buffers
-  if (!(a.nu1 == 1 && a.nu2 == 1 && !a.q2)) {
+  const bool fast = FIX65 || (a.nu1 == 1 && a.nu2 == 1 && !a.q2);
+  if (!fast) {
     for (int i = tid; i < 3 * tot; i += kTailThreads) va[i] = T(0);
     FEA_TAIL_SYNC();  // the zero fill must land before f_t is staged into the same region
   }
-  const bool fast = a.nu1 == 1 && a.nu2 == 1 && !a.q2;
   if (MULTI || !fast) {  // (the single-pattern fast path keeps its tables in registers)
     const int nt = MULTI ? a.ntab : 1;
     for (int i = tid; i < nt * kTS; i += kTailThreads) {
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     for (int i = tid; i < tot; i += kTailThreads) pl[i] = a.pid[i];
   const int wv = tid >> 6, lane = tid & 63;  // wave = row group, lane = column (Wt <= 65)
   constexpr int kWaves = kTailThreads / 64;
-  if (!fast || nlev == 1) {
+  if (!fast || (!FIX65 && nlev == 1)) {
     const T* src = a.f_t + (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1);
     constexpr int kRows = (kTailMaxN + kWaves - 1) / kWaves;  // rows per wave, all loads in flight at once
     T buf[kRows], b64[kRows];
@@ -478,22 +481,23 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
       if (r < Ht && lane == 0 && Wt == 65) fs[r * Wt + 64] = b64[i];
     }
   }
-  if (fast) {
+  if constexpr (FIX65) {
     // the first down phase reads f_t from HBM itself and stages it for the up phase; single pattern:
     // the tables come from uniform loads, so nothing has to land before it
+    if (MULTI) FEA_TAIL_SYNC();
+    tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+#ifdef FEA_TAIL_TRACE
+                               , nph
+#endif
+    );
+    return;
+  } else if (fast) {
     if (MULTI || nlev == 1) FEA_TAIL_SYNC();
-    if (a.Ht == 65 && a.Wt == 65 && nlev == 6)  // the tail of every BASELINE configuration
-      tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+    tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
 #ifdef FEA_TAIL_TRACE
-                                 , nph
+                        , nph
 #endif
-      );
-    else
-      tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
-#ifdef FEA_TAIL_TRACE
-                          , nph
-#endif
-      );
+    );
     return;
   }
   FEA_TAIL_SYNC();
@@ -654,8 +658,12 @@ static inline bool tail_dim_ok(int n, int nlev) {
     if (tail_lds_bytes<T>(Ht, Wt, nlev, multi) > kTailLdsBytes) return FEA_EINVAL;                           \
     TailArgs<T> a{f_t, v_t, pid_levels, ktab, omd, rtab, ptab, w0, w1, Ht, Wt, nlev, ld_t, bs_t, ntab, nu1, nu2,  \
                   q2};                                                                                        \
-    if (multi) k_mg_coarse_tail<T, true><<<B, kTailThreads, 0, (hipStream_t)stream>>>(a);                     \
-    else k_mg_coarse_tail<T, false><<<B, kTailThreads, 0, (hipStream_t)stream>>>(a);                          \
+    const bool fix65 = Ht == 65 && Wt == 65 && nlev == 6 && nu1 == 1 && nu2 == 1 && !q2;                     \
+    hipStream_t s_ = (hipStream_t)stream;                                                                     \
+    if (multi && fix65) k_mg_coarse_tail<T, true, true><<<B, kTailThreads, 0, s_>>>(a);                       \
+    else if (multi) k_mg_coarse_tail<T, true><<<B, kTailThreads, 0, s_>>>(a);                                  \
+    else if (fix65) k_mg_coarse_tail<T, false, true><<<B, kTailThreads, 0, s_>>>(a);                          \
+    else k_mg_coarse_tail<T, false><<<B, kTailThreads, 0, s_>>>(a);                                            \
     FEA_LAUNCH_CHECK();                                                                                       \
   }
 

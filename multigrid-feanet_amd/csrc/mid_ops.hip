@@ -416,9 +416,19 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
 // ---------------------------------------------------------------------------------------------
 // up: u_{a+k}, f_a .. f_{a+k-1} -> u_a
 // ---------------------------------------------------------------------------------------------
+// The up pass's per-level geometry (regions and LDS carve offsets), kept in LDS: every level reloads its
+// own after the barrier in front of it, so none of it is live across the levels (held in registers through
+// the unrolled level loop it pushed the two-material kernels past 128 VGPRs: scratch spills reloaded at
+// every barrier).
+struct MidUpGeo {
+  Reg u[kMidMaxK + 1];
+  int fx[kMidMaxK], uo[kMidMaxK + 1], po[kMidMaxK + 1], ko;
+};
+
 template <typename T, bool MULTI, int K>
 __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kMidLdsBytes];
+  __shared__ MidUpGeo geo;
   FEA_MID_MARK(2 * blockIdx.x);
   constexpr int OFF = 128 / (int)sizeof(T) - 1;
   constexpr int k = K;
@@ -450,10 +460,10 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
   }
   T* X = p;
   p += xmax;
-  T* ktb = p;
-  T* xtb = ktb + FEA_MAX_PATTERNS * kMS;
+  T* ktb0 = p;
+  T* xtb0 = ktb0 + FEA_MAX_PATTERNS * kMS;
   uint8_t* P[kMidMaxK + 1];
-  uint8_t* q = reinterpret_cast<uint8_t*>(xtb + FEA_MAX_PATTERNS * kMS);
+  uint8_t* q = reinterpret_cast<uint8_t*>(xtb0 + FEA_MAX_PATTERNS * kMS);
 #pragma unroll
   for (int j = 0; j <= k; ++j) {
     P[j] = q;
@@ -479,16 +489,26 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
     stage_batch<T, k + 1>(jf);
     FEA_MID_WAVE_MARK(1);
   }
-  tables_commit<T>(tl, ktb, xtb, a.ntab, a.nx);
+  tables_commit<T>(tl, ktb0, xtb0, a.ntab, a.nx);
+  if (MULTI && threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j <= k; ++j) {
+      geo.u[j] = u[j];
+      if (j < k) geo.fx[j] = (int)(Fx[j] - reinterpret_cast<T*>(smem));
+      if (j > 0) geo.uo[j] = (int)(U[j] - reinterpret_cast<T*>(smem));
+      geo.po[j] = (int)(P[j] - reinterpret_cast<uint8_t*>(smem));
+    }
+    geo.ko = (int)(ktb0 - reinterpret_cast<T*>(smem));
+  }
   FEA_MID_SYNC(0);
   T ks[9], ps[9], om = T(0);
   if constexpr (!MULTI) {
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-      ks[d] = ktb[d];
-      ps[d] = xtb[d];
+      ks[d] = ktb0[d];
+      ps[d] = xtb0[d];
     }
-    om = ktb[9];
+    om = ktb0[9];
   }
 
   // Per level: wave w owns a contiguous block of u-region rows; for each chunk of <= 4 of them it forms
@@ -500,14 +520,24 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = k - 1; j >= 0; --j) {
-    const Reg x = xreg(j), C = u[j + 1];
+    // this level's geometry, from LDS (see MidUpGeo)
+    // (LDS loads are not known to be uniform: readfirstlane puts the values back into scalar registers)
+    auto rfl = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+    auto greg = [&](int i) { return Reg{rfl(geo.u[i].r0), rfl(geo.u[i].c0), rfl(geo.u[i].nr), rfl(geo.u[i].nc)}; };
+    // (single pattern: few enough registers to keep it all live, which is faster)
+    T* const sb = reinterpret_cast<T*>(smem);
+    const uint8_t* const sp = reinterpret_cast<const uint8_t*>(smem);
+    const Reg U0 = MULTI ? greg(j) : u[j], C = MULTI ? greg(j + 1) : u[j + 1];
+    const Reg x = Reg{U0.r0 - 1, U0.c0 - 1, U0.nr + 2, U0.nc + 2};
     const int H = a.H[j], W = a.W[j];
-    const T* f = Fx[j];
-    const T* e = U[j + 1];
-    const uint8_t* pj = P[j];
-    const uint8_t* pc = P[j + 1];
+    const T* f = MULTI ? sb + rfl(geo.fx[j]) : Fx[j];
+    const T* e = MULTI ? sb + rfl(geo.uo[j + 1]) : U[j + 1];
+    const uint8_t* pj = MULTI ? sp + rfl(geo.po[j]) : P[j];
+    const uint8_t* pc = MULTI ? sp + rfl(geo.po[j + 1]) : P[j + 1];
+    const T* ktb = MULTI ? sb + rfl(geo.ko) : ktb0;
+    const T* xtb = ktb + FEA_MAX_PATTERNS * kMS;
     // the coarse pattern map region: x region of level j+1 (j+1 < k) or its u region (j+1 == k)
-    const Reg PC = (j + 1 < k) ? xreg(j + 1) : u[k];
+    const Reg PC = (j + 1 < k) ? Reg{C.r0 - 1, C.c0 - 1, C.nr + 2, C.nc + 2} : C;
     // row-wave form (regions <= 64 columns): lane = column x.c0 + lane
     const int c = x.c0 + lane;
     const bool lv = lane < x.nc;
@@ -519,8 +549,7 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
     const int iL = min(max(cL - C.c0, 0), C.nc - 1), iR = min(max(cR - C.c0, 0), C.nc - 1);
     const int qL = min(max(cL - PC.c0, 0), PC.nc - 1), qR = min(max(cR - PC.c0, 0), PC.nc - 1);
     const bool codd = (c & 1) != 0;
-    const Reg U0 = u[j];
-    T* un = j > 0 ? U[j] : nullptr;
+    T* un = j > 0 ? (MULTI ? sb + rfl(geo.uo[j]) : U[j]) : nullptr;
     T* go = j == 0 ? a.out + (long long)b * a.bs[0] : nullptr;
     const bool lo = lane >= 1 && lane <= U0.nc;  // u-region column c = U0.c0 + lane - 1
     auto rows = [&](auto par_c, auto per_c, int yy0, int yy1) {
