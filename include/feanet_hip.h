@@ -235,6 +235,21 @@ int fea_mg_residual_restrict_f64(const double* u, const double* f, double* v_out
                                  const double* rtab, int nrtab, double w0, int B, int H, int W, int ld,
                                  long long bstride, int ldc, long long bstridec, void* stream);
 
+/* Two zero-guess restrictions in one pass (the first two levels below the finest going down):
+ *   v = omd*f;  fc = w0*R(f - K v);  v' = omd*fc;  fc2 = w0*R(fc - K v')     (interiors)
+ * fc (the H_c x W_c level, pitch ldc / bstridec) is stored as well — the up pass recomputes v' from it —
+ * and fc2 (pitch ldc2 / bstridec2) is the level below.  Bitwise the two fea_mg_residual_restrict calls
+ * with u = v_out = NULL.  FEANet/multigrid.py:171-172 then :168-170 at two consecutive levels
+ * (MultiGrid.Step's recursion, mg_test :27352-27363).  pidc: the coarse level's pattern map (ntab > 1). */
+int fea_mg_zero_restrict2_f32(const float* f, float* fc, float* fc2, const uint8_t* pid, const uint8_t* pidc,
+                              const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
+                              float w0, int B, int H, int W, int ld, long long bstride, int ldc,
+                              long long bstridec, int ldc2, long long bstridec2, void* stream);
+int fea_mg_zero_restrict2_f64(const double* f, double* fc, double* fc2, const uint8_t* pid, const uint8_t* pidc,
+                              const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
+                              double w0, int B, int H, int W, int ld, long long bstride, int ldc,
+                              long long bstridec, int ldc2, long long bstridec2, void* stream);
+
 /* Fused pre-smooth + residual + restriction on a level with a given iterate (temporal blocking):
  *   u_out = J(u, f) (interior)   and   fc(interior) = w0 * R(f - K u_out)
  * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357).

@@ -248,6 +248,8 @@ struct MgArgs {
   long long bs;
   int Hc, Wc, ldc;
   long long bsc;
+  int Hc2, Wc2, ldc2;  // the level below the coarse one (k_mg_zero_restrict2: its right-hand side in out2)
+  long long bsc2;
   int nstrips, ntr;  // strips per row, row tasks per sample
   int rb;            // fine rows per row task (even)
   int rlo, rhi;      // row range of the residual norm
@@ -1059,6 +1061,277 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Two zero-guess restrictions in one pass (levels l and l+1 going down, both below the tail-free top):
+//   v = omd f_l;  f_{l+1} = w0 R(f_l - K v);  v' = omd f_{l+1};  f_{l+2} = w0 R(f_{l+1} - K v')
+// Overlapped strips as k_mg_zero_restrict, with a second stage on the coarse values the first one leaves
+// in registers (one per lane in fp64, two in fp32; neighbours by DPP): f_{l+1} is still stored (the up
+// pass recomputes v' from it) but never re-read, and the level-(l+1) launch disappears.  Each strip
+// loads HLc = max(V, 4) columns left of the S2 it owns, so the second stage's values are exact on its owned
+// columns; a row task owns rb/4 rows of f_{l+2} and recomputes the 3 rows of f_{l+1} above and the 1 below
+// them.  Every node value is the same expression, in the same order, as the two single-level launches
+// (bitwise: tests/test_gpu_mg.py::test_zero_restrict2_bitwise).
+// ---------------------------------------------------------------------------
+template <typename T>
+struct Ovl2 {
+  static constexpr int V = Frame<T>::VEC;
+  static constexpr int Q = V / 2;
+  static constexpr int HLC = V > 4 ? V : 4;                  // left halo columns (a multiple of V)
+  static constexpr int S = ((64 * V - 6 - HLC) / 4) * 4;     // owned fine columns per strip (fp64 116, fp32 244)
+};
+
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
+  using F = Frame<T>;
+  using O = Ovl2<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = O::Q;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc, Hc2 = g.Hc2, Wc2 = g.Wc2;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column
+  const int cs = c0 - O::HLC;      // first loaded column
+  const int cl = cs + V * lane;
+  const int J0 = (cl + 1) / 2;     // the lane's first coarse column (level l+1)
+  // owned columns of f_{l+1} and f_{l+2}, owned rows of f_{l+2}
+  const int Jlo = id.s * (O::S / 2) + 1, Jhi = Jlo + O::S / 2;
+  const int Mlo = id.s * (O::S / 4) + 1, Mhi = Mlo + O::S / 4;
+  const int K0 = 1 + id.t * (g.rb / 4);
+  const int K1 = min(K0 + g.rb / 4, Hc2 - 1);
+  const int Ilo = 2 * K0 - 1, Ihi = K1 == Hc2 - 1 ? Hc - 1 : 2 * K1 - 1;  // owned rows of f_{l+1}
+  T ks[9], rs[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      rs[d] = g.rtab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w0 = g.w;
+  bool cin[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  bool jin[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) jin[q] = J0 + q >= 1 && J0 + q <= Wc - 2;
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const T* __restrict__ fb = g.f + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  const uint8_t* __restrict__ pcb = MULTI ? g.pidc + F::OFF + J0 : nullptr;
+  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
+  T* __restrict__ cb2 = g.out2 + (long long)id.b * g.bsc2 + F::OFF;
+  const int ld = g.ld;
+  const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the grid re-read the last needed line
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+
+  // ---- stage 1 (level l): the rows of k_mg_zero_restrict
+  struct In {
+    T f[V];
+    int p[V];
+  };
+  struct Wn {
+    Row<T, V> v;
+    T f[V];
+    PRow<V> p;
+  };
+  auto load = [&](int y) {
+    In r;
+    const long long o = rowo(y);
+    vload<T, V>(fb + o, r.f);
+    if constexpr (MULTI) pload<V>(pb + o, r.p);
+    return r;
+  };
+  auto mk = [&](const In& r, int y) {
+    Wn w;
+    const bool rin = y >= 1 && y <= H - 2;
+    T x[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T omk = MULTI ? tab[r.p[k] * kTabStride + 9] : om;
+      x[k] = (rin && cin[k]) ? omk * r.f[k] : T(0);
+      w.f[k] = r.f[k];
+    }
+    w.v = own_row<T, V>(x);
+    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    return w;
+  };
+  auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) r[k] = b.f[k] - kapply<T, V, MULTI>(a.v, b.v, c.v, a.p, b.p, c.p, k, ks, tab);
+    r[V] = shl1(r[0], T(0));
+  };
+
+  // ---- stage 2 (level l+1): v' window rows I-2, I-1, I; residual rows of the current coarse-row pair
+  Row<T, Q> Va{}, Vb{}, Vc{};
+  PRow<Q> Qa{}, Qb{}, Qc{};
+  T fp2[Q];  // f_{l+1} of the previous row
+  Row<T, Q> Ro{}, Re{};  // the last odd and even residual rows of level l+1 (2K-1, 2K while row K forms)
+  PRow<Q> So{}, Se{};    // their patterns
+#pragma unroll
+  for (int q = 0; q < Q; ++q) fp2[q] = T(0);
+
+  // push f_{l+1} row I (all lanes, exact on the valid ones); n = rows pushed before it
+  // ODD: parity of I, a compile-time constant (Ia is even), so the residual-row rotation below is static
+  auto push = [&](int I, const T (&o)[Q], int n, auto odd_c) {
+    constexpr bool ODD = decltype(odd_c)::value;
+    int pq[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) pq[q] = 0;
+    if constexpr (MULTI) {
+      const int Ic = min(max(I, -1), Hc);
+      pload<Q>(pcb + (long long)(Ic + 1) * g.ldc, pq);
+    }
+    T x[Q];
+    const bool iin = I >= 1 && I <= Hc - 2;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const T omk = MULTI ? tab[pq[q] * kTabStride + 9] : om;
+      x[q] = (iin && jin[q]) ? omk * o[q] : T(0);
+    }
+    Va = Vb;
+    Vb = Vc;
+    Vc = own_row<T, Q>(x);
+    if constexpr (MULTI) {
+      Qa = Qb;
+      Qb = Qc;
+      Qc = own_prow<Q>(pq);
+    }
+    if (n >= 2) {
+      // residual row I-1 of level l+1 (k_mg_zero_restrict's resid on the coarse values)
+      T r[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) r[q] = fp2[q] - kapply<T, Q, MULTI>(Va, Vb, Vc, Qa, Qb, Qc, q, ks, tab);
+      const Row<T, Q> R = own_row<T, Q>(r);
+      const int j = I - 1;  // residual row index (odd when I is even)
+      if constexpr (!ODD) {
+        // j = 2K+1 closes f_{l+2} row K (residual rows 2K-1 = Ro, 2K = Re, 2K+1 = R)
+        const int K = (j - 1) / 2;
+        if (K >= K0 && K < K1) {
+          // one output column per lane: fp64 the lane's own column when it is even, fp32 its second one
+          constexpr int B0 = Q == 1 ? 0 : 1;     // window index of column 2M-1
+          const int Jm = J0 + (Q == 1 ? 0 : 1);  // column 2M
+          const int M = Jm / 2;
+          T acc;
+          if constexpr (!MULTI) {
+            acc = rs[0] * Ro.a[B0];
+            acc += rs[1] * Ro.a[B0 + 1];
+            acc += rs[2] * Ro.a[B0 + 2];
+            acc += rs[3] * Re.a[B0];
+            acc += rs[4] * Re.a[B0 + 1];
+            acc += rs[5] * Re.a[B0 + 2];
+            acc += rs[6] * R.a[B0];
+            acc += rs[7] * R.a[B0 + 1];
+            acc += rs[8] * R.a[B0 + 2];
+          } else {
+            acc = rtb[So.a[B0] + 0] * Ro.a[B0];
+            acc += rtb[So.a[B0 + 1] + 1] * Ro.a[B0 + 1];
+            acc += rtb[So.a[B0 + 2] + 2] * Ro.a[B0 + 2];
+            acc += rtb[Se.a[B0] + 3] * Re.a[B0];
+            acc += rtb[Se.a[B0 + 1] + 4] * Re.a[B0 + 1];
+            acc += rtb[Se.a[B0 + 2] + 5] * Re.a[B0 + 2];
+            acc += rtb[Qb.a[B0] + 6] * R.a[B0];
+            acc += rtb[Qb.a[B0 + 1] + 7] * R.a[B0 + 1];
+            acc += rtb[Qb.a[B0 + 2] + 8] * R.a[B0 + 2];
+          }
+          if (!(Jm & 1) && M >= Mlo && M < Mhi && M <= Wc2 - 2) cb2[(long long)(K + 1) * g.ldc2 + M] = w0 * acc;
+        }
+        Ro = R;
+        if constexpr (MULTI) So = Qb;
+      } else {
+        Re = R;
+        if constexpr (MULTI) Se = Qb;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) fp2[q] = o[q];
+  };
+
+  const int Ia = 2 * K0 - 2, Ib = 2 * K1;  // f_{l+1} rows computed (Ia .. Ib inclusive)
+  const int y0 = 2 * Ia - 1;
+  Wn X0 = mk(load(y0 - 1), y0 - 1);
+  Wn X1 = mk(load(y0), y0);
+  Wn X2 = mk(load(y0 + 1), y0 + 1);
+  T Ra[V + 1], Rb[V + 1], Rc[V + 1];
+  PRow<V> Pa = X1.p, Pb, Pc;
+  resid(X0, X1, X2, Ra);
+  // the two fine rows of a coarse row are loaded two coarse rows ahead, in ring slots indexed by the
+  // row's parity (compile-time), as in k_mg_zero_restrict
+  In ring[2][2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    ring[d][0] = load(2 * Ia + 1 + 2 * d);
+    ring[d][1] = load(2 * Ia + 2 + 2 * d);
+  }
+  auto row = [&](int I, int n, auto odd_c) {
+    constexpr int SL = decltype(odd_c)::value ? 1 : 0;
+    X0 = X1;  // fine row 2I
+    X1 = X2;
+    X2 = mk(ring[SL][0], 2 * I + 1);
+    ring[SL][0] = load(2 * I + 5);
+    resid(X0, X1, X2, Rb);
+    Pb = X1.p;
+    X0 = X1;  // fine row 2I+1
+    X1 = X2;
+    X2 = mk(ring[SL][1], 2 * I + 2);
+    ring[SL][1] = load(2 * I + 6);
+    resid(X0, X1, X2, Rc);
+    Pc = X1.p;
+    T o[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      T acc;
+      if constexpr (!MULTI) {
+        acc = rs[0] * Ra[2 * q];
+        acc += rs[1] * Ra[2 * q + 1];
+        acc += rs[2] * Ra[2 * q + 2];
+        acc += rs[3] * Rb[2 * q];
+        acc += rs[4] * Rb[2 * q + 1];
+        acc += rs[5] * Rb[2 * q + 2];
+        acc += rs[6] * Rc[2 * q];
+        acc += rs[7] * Rc[2 * q + 1];
+        acc += rs[8] * Rc[2 * q + 2];
+      } else {
+        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
+        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
+        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
+        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
+        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
+        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
+        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
+        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
+        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+      }
+      o[q] = w0 * acc;
+    }
+    // f_{l+1}: owned rows and columns only
+    if (I >= Ilo && I < Ihi) {
+      T* cp = cb + (long long)(I + 1) * g.ldc;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (J0 + q >= Jlo && J0 + q < Jhi && J0 + q <= Wc - 2) cp[q] = o[q];
+    }
+    push(I, o, n, odd_c);
+#pragma unroll
+    for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
+    Pa = Pc;
+  };
+  // Ib - Ia + 1 = 2 (K1 - K0) + 3 rows: pairs (even, odd), then the last (even) row
+  int n = 0, I = Ia;
+  for (; I + 1 <= Ib; I += 2, n += 2) {
+    row(I, n, std::false_type{});
+    row(I + 1, n + 1, std::true_type{});
+  }
+  row(I, n, std::false_type{});
+}
+
 // Kernel C: fused prolongation + correction (+ post-sweep):
 //   v = u + w1 * P(ec)   (P kernel of the coarse node);   out = SWEEP ? J(v, f) : v
 // ZU (with SWEEP): the level's iterate is its zero-guess pre-sweep u = omd*f (interior, 0 on the
@@ -2452,3 +2725,54 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
 #define COMMA ,
 FEA_MG_API(f32, float)
 FEA_MG_API(f64, double)
+
+// Rows per task of k_mg_zero_restrict2 (fine rows, a multiple of 4): the tallest power of two that still
+// gives kZr2Waves waves, at least kZr2MinRb (each task recomputes 3 + 1 rows of the intermediate level).
+// Lab A/B at 2049^2 fp64 (tools/lab/zr2_ab.py): 16 rows 14.3 us, 32 rows 16.2, 64 rows 19.1.
+#ifndef FEA_ZR2_MINRB
+#define FEA_ZR2_MINRB 4
+#endif
+#ifndef FEA_ZR2_WAVES
+#define FEA_ZR2_WAVES 2048
+#endif
+constexpr int kZr2MinRb = FEA_ZR2_MINRB;
+constexpr int kZr2Waves = FEA_ZR2_WAVES;
+
+template <typename T>
+static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const uint8_t* pidc, const T* ktab,
+                          const T* omd, int ntab, const T* rtab, int nrtab, T w0, int B, int H, int W, int ld,
+                          long long bs, int ldc, long long bsc, int ldc2, long long bsc2, void* stream) {
+  if (!f || !fc || !fc2 || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;
+  if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  if (!coarse_ok<T>(Hc, Wc, ldc2, bsc2)) return FEA_EINVAL;
+  const bool multi = ntab > 1;
+  if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (multi && (!pid || !pidc))) return FEA_EINVAL;
+  if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;
+  if (multi && nrtab == 1) return FEA_EINVAL;
+  MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);
+  g.f = f; g.out = fc; g.out2 = fc2; g.pid = pid; g.pidc = pidc; g.ktab = ktab; g.omd = omd; g.ntab = ntab;
+  g.rtab = rtab; g.nrtab = nrtab; g.w = w0;
+  g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;
+  g.Hc2 = (Hc + 1) / 2; g.Wc2 = (Wc + 1) / 2; g.ldc2 = ldc2; g.bsc2 = bsc2;
+  g.nstrips = div_up(W - 2, Ovl2<T>::S);
+  g.rb = 2 * kRB;
+  while (g.rb > kZr2MinRb && (long long)B * g.nstrips * div_up(g.Hc2 - 2, g.rb / 4) < kZr2Waves) g.rb /= 2;
+  g.ntr = div_up(g.Hc2 - 2, g.rb / 4);
+  const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);
+  hipStream_t s = (hipStream_t)stream;
+  if (multi) k_mg_zero_restrict2<T, true><<<grid, 256, 0, s>>>(g);
+  else k_mg_zero_restrict2<T, false><<<grid, 256, 0, s>>>(g);
+  FEA_LAUNCH_CHECK();
+}
+
+#define FEA_ZR2_API(SUF, T)                                                                                   \
+  extern "C" int fea_mg_zero_restrict2_##SUF(const T* f, T* fc, T* fc2, const uint8_t* pid, const uint8_t* pidc, \
+                                             const T* ktab, const T* omd, int ntab, const T* rtab, int nrtab,     \
+                                             T w0, int B, int H, int W, int ld, long long bs, int ldc,          \
+                                             long long bsc, int ldc2, long long bsc2, void* stream) {            \
+    return zero_restrict2<T>(f, fc, fc2, pid, pidc, ktab, omd, ntab, rtab, nrtab, w0, B, H, W, ld, bs, ldc, bsc,  \
+                             ldc2, bsc2, stream);                                                              \
+  }
+FEA_ZR2_API(f32, float)
+FEA_ZR2_API(f64, double)

@@ -42,6 +42,7 @@ _SIGS = {
     "mg_unpack": [P, P, I, I, I, I, LL, P],
     "mg_sweep": [P, P, P, P, P, P, I, I, I, I, I, LL, P],
     "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_zero_restrict2": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P],
     "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P, P, P, P],
     "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, I, LL, I, LL, P],

@@ -176,6 +176,25 @@ def hjac_schedule(L, nu1=1, nu2=1, start="a"):
     return steps, cur[0]
 
 
+def pair_restrictions(steps, can_pair):
+    """Rewrite two consecutive single-level zero-guess restrictions (("resid_restrict", l, None, None), then
+    the same at l + 1) into one ("resid_restrict2", l) step — fea_mg_zero_restrict2, bitwise the two —
+    where can_pair(l) allows it.  Run after group_mid (the levels it leaves to single-level launches)."""
+    out = []
+    i = 0
+    zr = lambda st: st[0] == "resid_restrict" and st[2] is None and st[3] is None
+    while i < len(steps):
+        st = steps[i]
+        if (zr(st) and i + 1 < len(steps) and zr(steps[i + 1]) and steps[i + 1][1] == st[1] + 1
+                and can_pair(st[1])):
+            out.append(("resid_restrict2", st[1]))
+            i += 2
+            continue
+        out.append(st)
+        i += 1
+    return out
+
+
 def group_mid(steps, pick_down, pick_up):
     """Rewrite runs of consecutive zero-guess restrictions (("resid_restrict", l, None, None), l
     ascending) and of recomputed prolongations (("prolong_sweep", l, OMDF, csrc, dst), l descending)

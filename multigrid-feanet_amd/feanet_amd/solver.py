@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import OMDF, group_mid, hjac_schedule, vcycle_schedule
+from .schedule import OMDF, group_mid, hjac_schedule, pair_restrictions, vcycle_schedule
 
 
 _SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
@@ -119,6 +119,8 @@ class MultigridSolver:
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
         mid: run latency-bound coarse levels (B*H*W <= MID_NODES) up to four per launch
             (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels).
+        pair_down: two consecutive zero-guess restrictions left to single-level launches run as one
+            (fea_mg_zero_restrict2, bitwise the two).
     """
 
     MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
@@ -129,7 +131,7 @@ class MultigridSolver:
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None, join_cycles=True, mid=True):
+                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_down=True):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -162,6 +164,7 @@ class MultigridSolver:
         self.zero_start = zero_start
         self.join_cycles = join_cycles
         self.mid = bool(mid)
+        self.pair_down = bool(pair_down)
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -367,6 +370,9 @@ class MultigridSolver:
                                          top_zero=self.zero_start)
             if self.mid:
                 steps = group_mid(steps, lambda lv: self._pick_mid(lv, False), lambda lv: self._pick_mid(lv, True))
+            if self.pair_down:
+                steps = pair_restrictions(steps, lambda l: l + 2 < self.L and self.levels[l + 2].H >= 3
+                                          and self.levels[l + 2].W >= 3)
         return [self.bind_step(st) for st in steps], end
 
     def _mid_tile(self, up, a, k):
@@ -442,6 +448,9 @@ class MultigridSolver:
         if kind == "resid_restrict":
             return ("mg_residual_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
                                              kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l))
+        if kind == "resid_restrict2":
+            return ("mg_zero_restrict2", (f, lv[l + 1].f.data_ptr(), lv[l + 2].f.data_ptr(), pid(l), pid(l + 1),
+                                          kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l) + cgeom(l + 1))
         if kind == "sweep_restrict":
             return ("mg_sweep_restrict", (ptr(l, st[2]), f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l),
                                           kt, om, nt, rt, nr, self.w[0]) + geom(l) + cgeom(l) + (None, None, None))
@@ -922,6 +931,14 @@ class MultigridSolver:
                     total += esz * sum(sizes) + pb * sum(sizes[:-1])
                 else:  # read f_a..f_{a+k-1}, u_{a+k}; write u_a
                     total += esz * (sum(sizes) + sizes[0]) + pb * sum(sizes)
+                continue
+            if name == "mg_zero_restrict2":  # read f_l (+ pattern), write f_{l+1}, f_{l+2}
+                B, H, W = args[-9:-6]
+                n0 = B * (H - 2) * (W - 2)
+                H, W = (H + 1) // 2, (W + 1) // 2
+                n1 = B * (H - 2) * (W - 2)
+                n2 = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
+                total += n0 * (esz + pb) + (n1 + n2) * esz
                 continue
             if name == "mg_sweep_restrict":  # (..., B, H, W, ld, bs, ldc, bsc, norm_ws, norm_hist, norm_cnt)
                 B, H, W = args[-10:-7]

@@ -1034,3 +1034,65 @@ def test_zero_guess_kernel_variants_bitwise(T, problem, n, m, B, monkeypatch):
     ps = [run("ps", small_nt=True), run("ps")]
     assert np.array_equal(ps[0], ps[1])
     assert (ps[0][:, 0, :] == 7).all() and (ps[0][:, :, -1] == 7).all()
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n,m,B", [("poisson", 8, None, 1), ("poisson", 16, None, 3), ("poisson", 64, None, 2),
+                                           ("poisson", 256, None, 1), ("poisson", 512, None, 2),
+                                           ("poisson", 2048, None, 1), ("poisson", 256, 64, 2),
+                                           ("poisson", 64, 512, 1), ("poisson", 488, 120, 1),
+                                           ("interface", 32, None, 3), ("interface", 256, None, 1),
+                                           ("interface", 1024, None, 1)])
+def test_zero_restrict2_bitwise(T, problem, n, m, B):
+    """fea_mg_zero_restrict2 (two zero-guess restrictions in one pass) is bitwise the two single-level
+    k_mg_zero_restrict launches it replaces — both outputs, every size (strip and task edges, rows != columns,
+    one to several strips and row tasks), batch, dtype, and the two-material problem with per-pattern learned
+    R; boundary nodes of both outputs are left untouched."""
+    from feanet_amd import _lib
+    rng = np.random.default_rng(7 * n + B)
+    m_ = n if m is None else m
+    fr = Frame(n, B, T, problem, m=m)
+    c1 = Frame(n // 2, B, T, problem, m=m_ // 2)
+    c2 = Frame(n // 4, B, T, problem, m=m_ // 4)
+    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned=problem == "interface")
+    nt = ktab.shape[0]
+    _, f = rand_state(rng, B, (fr.H, fr.W), T)
+    fr.put("f", f)
+    s1 = np.full((B, c1.H, c1.W), 3.0)
+    s2 = np.full((B, c2.H, c2.W), 5.0)
+    c1.put("f", s1)
+    c2.put("f", s2)
+    _lib.call("mg_residual_restrict", T, None, fr.L.f.data_ptr(), None, c1.L.f.data_ptr(), fr.pid(), kt.data_ptr(),
+              om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *fr.args(), c1.L.ld, c1.L.bs, None)
+    _lib.call("mg_residual_restrict", T, None, c1.L.f.data_ptr(), None, c2.L.f.data_ptr(), c1.pid(), kt.data_ptr(),
+              om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *c1.args(), c2.L.ld, c2.L.bs, None)
+    ref1, ref2 = c1.get("f"), c2.get("f")
+    c1.put("f", s1)
+    c2.put("f", s2)
+    _lib.call("mg_zero_restrict2", T, fr.L.f.data_ptr(), c1.L.f.data_ptr(), c2.L.f.data_ptr(), fr.pid(), c1.pid(),
+              kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *fr.args(), c1.L.ld, c1.L.bs, c2.L.ld,
+              c2.L.bs, None)
+    got1, got2 = c1.get("f"), c2.get("f")
+    assert np.array_equal(got1, ref1), f"f_l+1: {np.argwhere(got1 != ref1)[:5]}"
+    assert np.array_equal(got2, ref2), f"f_l+2: {np.argwhere(got2 != ref2)[:5]}"
+    assert (got1[:, 0, :] == 3).all() and (got1[:, :, -1] == 3).all()
+    assert (got2[:, -1, :] == 5).all() and (got2[:, :, 0] == 5).all()
+
+
+def test_solver_pairs_restrictions():
+    """The solver's plan at 4097^2 runs levels 1 and 2 going down as ONE fea_mg_zero_restrict2 launch, and the
+    V-cycle with and without the pairing is bitwise the same."""
+    from feanet_amd.solver import MultigridSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    f = torch.randn(1, 1, 4097, 4097, dtype=torch.float64, device="cuda", generator=g)
+    outs = []
+    for pair in (True, False):
+        s = MultigridSolver(4096, dtype=torch.float64, pair_down=pair)
+        names = [nm for nm, _ in s._plan("a")[0]]
+        assert ("mg_zero_restrict2" in names) == pair, names
+        s.set_rhs(f=f)
+        s.load()
+        s.vcycle(3)
+        outs.append(s.solution())
+    assert torch.equal(outs[0], outs[1])
