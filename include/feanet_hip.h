@@ -279,6 +279,22 @@ int fea_mg_prolong_sweep_f64(const double* u, const double* ec, const double* f,
                              int ntab, const double* ptab, int nptab, double w1, int B, int H, int W, int ld,
                              long long bstride, int ldc, long long bstridec, void* stream);
 
+/* Two recomputed-iterate prolongations + post-sweeps in one pass (the first two levels below the
+ * multi-level launch going up):
+ *   x' = omd*fc + w1*P(ec2);  u' = J(x', fc);  x = omd*f + w1*P(u');  out = J(x, f)     (interiors)
+ * fc / pidc: the coarse level's right-hand side and pattern map (pitch ldc / bstridec), ec2 / pidc2: the
+ * correction and pattern map of the level below it (pitch ldc2 / bstridec2).  u' is never stored.  Bitwise
+ * fea_mg_prolong_sweep(u = NULL) on the coarse level, then on this one.  FEANet/multigrid.py:177-181 at two
+ * consecutive levels (MultiGrid.Step's recursion unwinding, mg_test :27364-27372). */
+int fea_mg_prolong2_f32(const float* fc, const float* ec2, const float* f, float* out, const uint8_t* pid,
+                        const uint8_t* pidc, const uint8_t* pidc2, const float* ktab, const float* omd, int ntab,
+                        const float* ptab, int nptab, float w1, int B, int H, int W, int ld, long long bstride,
+                        int ldc, long long bstridec, int ldc2, long long bstridec2, void* stream);
+int fea_mg_prolong2_f64(const double* fc, const double* ec2, const double* f, double* out, const uint8_t* pid,
+                        const uint8_t* pidc, const uint8_t* pidc2, const double* ktab, const double* omd, int ntab,
+                        const double* ptab, int nptab, double w1, int B, int H, int W, int ld, long long bstride,
+                        int ldc, long long bstridec, int ldc2, long long bstridec2, void* stream);
+
 /* Cycle join (temporal blocking across two V-cycles on one level): the post-smooth of cycle k and the
  * pre-smooth + residual + restriction of cycle k+1 in one pass —
  *   v = J(u + w1 * P(ec), f)  (not stored);   u_out = J(v, f);   fc(interior) = w0 * R(f - K u_out)

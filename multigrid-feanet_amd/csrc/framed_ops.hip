@@ -248,8 +248,10 @@ struct MgArgs {
   long long bs;
   int Hc, Wc, ldc;
   long long bsc;
-  int Hc2, Wc2, ldc2;  // the level below the coarse one (k_mg_zero_restrict2: its right-hand side in out2)
-  long long bsc2;
+  int Hc2, Wc2, ldc2;  // the level below the coarse one (k_mg_zero_restrict2: its right-hand side in out2;
+  long long bsc2;      //   k_mg_prolong2: its correction in ec2, its pattern map in pidc2)
+  const T* ec2;
+  const uint8_t* pidc2;
   int nstrips, ntr;  // strips per row, row tasks per sample
   int rb;            // fine rows per row task (even)
   int rlo, rhi;      // row range of the residual norm
@@ -1807,6 +1809,285 @@ __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
 }
 
 // ---------------------------------------------------------------------------
+// Two recomputed-iterate prolongations in one pass (levels l+1 and l going up, below the multi-level launch):
+//   x' = omd f_{l+1} + w1 P(e_{l+2});  u' = J(x', f_{l+1});  x = omd f_l + w1 P(u');  out = J(x, f_l)
+// k_mg_prolong_zu_ovl on level l, whose coarse correction rows u' come from a second stage on the coarse
+// values in registers (one per lane in fp64, two in fp32; neighbours by DPP) instead of a separate launch:
+// u' is never stored.  Each strip loads three lanes left of the S it owns, so the coarse stage is exact on
+// every lane the fine one reads; the coarse stage advances one row per two fine rows, its inputs in the same
+// prefetch ring.  Same per-node expressions and order as the two single-level launches (bitwise:
+// tests/test_gpu_mg.py::test_prolong2_bitwise).
+// ---------------------------------------------------------------------------
+template <typename T>
+struct Ovl4 {
+  static constexpr int V = Frame<T>::VEC;
+  static constexpr int HL = 3;          // lanes of left halo; owning lanes HL .. 61
+  static constexpr int S = 59 * V;      // owned fine columns per strip (fp64 118, fp32 236)
+};
+
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
+  using F = Frame<T>;
+  using O = Ovl4<T>;
+  constexpr int V = F::VEC;
+  constexpr int Q = V / 2;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, ptb, g.ptab, g.nptab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  const int lane = lane_id();
+  const int H = g.H, Hc = g.Hc, W = g.W, Wc = g.Wc, Hc2 = g.Hc2, Wc2 = g.Wc2;
+  const int c0 = 1 + id.s * O::S;  // first owned fine column
+  const int cs = c0 - O::HL * V;   // first loaded column (odd)
+  const int cl = cs + V * lane;
+  const int r0 = 1 + id.t * g.rb;  // odd
+  const int r1 = min(r0 + g.rb, H - 1);
+  T ks[9], ps[9];
+  T om = 0;
+  if constexpr (!MULTI) {
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      ps[d] = g.ptab[d];
+    }
+    om = g.omd[0];
+  }
+  const T w1 = g.w;
+  const int ld = g.ld, ldc = g.ldc, ldc2 = g.ldc2;
+  bool cin[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  const bool own = lane >= O::HL && lane < 64 - 2;
+  const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the grid re-read the last needed line
+  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const T* __restrict__ fb = g.f + boff;
+  T* __restrict__ ob = g.out + boff;
+  const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
+  const int jc = (cs + 1) / 2;   // coarse column of lane 0's first own coarse node
+  const int J0 = jc + Q * ll;    // this lane's first coarse column (the loaded one)
+  const T* __restrict__ f2b = g.ec + (long long)id.b * g.bsc + F::OFF + J0;  // f_{l+1} (in ec)
+  const uint8_t* __restrict__ p2b = MULTI ? g.pidc + F::OFF + J0 : nullptr;
+  bool jin[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) jin[q] = J0 + q >= 1 && J0 + q <= Wc - 2;
+  // level l+2 columns KL, KL+1 feed this lane's coarse columns (odd J: (J-1)/2, (J+1)/2; even J: J/2)
+  const int KL = min((J0 - 1) >> 1, Wc2 - 2);
+  const T* __restrict__ e3b = g.ec2 + (long long)id.b * g.bsc2 + F::OFF + KL;
+  const uint8_t* __restrict__ p3b = MULTI ? g.pidc2 + F::OFF + KL : nullptr;
+  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+  auto crowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc) + 1) * ldc; };
+  auto c2rowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc2) + 1) * ldc2; };
+
+  // ---- coarse stage (level l+1): x' and u' rows ----
+  struct In2 {  // inputs of x' row b: f_{l+1} (own coarse columns), patterns, e_{l+2} rows b>>1, (b>>1)+1
+    T f[Q];
+    int p[Q];
+    T e[2][2];
+    int pe[2][2];
+  };
+  auto ld2 = [&](int b) {
+    In2 r;
+    vload<T, Q>(f2b + crowo(b), r.f);
+    if constexpr (MULTI) pload<Q>(p2b + crowo(b), r.p);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long long o = c2rowo((b >> 1) + h);
+      r.e[h][0] = e3b[o];
+      r.e[h][1] = e3b[o + 1];
+      if constexpr (MULTI) {
+        r.pe[h][0] = p3b[o] * kTabStride;
+        r.pe[h][1] = p3b[o + 1] * kTabStride;
+      }
+    }
+    return r;
+  };
+  // crow_term on level l+2 values for coarse column Jq (bitwise k_mg_prolong_zu_ovl's coarse term)
+  auto term2 = [&](const T (&e)[2], const int (&pe)[2], int Jq, int ky) -> T {
+    if (Jq & 1) {  // odd: (Jq-1)/2 (kx = 2) and (Jq+1)/2 (kx = 0) — KL and KL+1
+      T t = (MULTI ? ptb[pe[0] + ky * 3 + 2] : ps[ky * 3 + 2]) * e[0];
+      t += (MULTI ? ptb[pe[1] + ky * 3 + 0] : ps[ky * 3 + 0]) * e[1];
+      return t;
+    }
+    return (MULTI ? ptb[pe[1] + ky * 3 + 1] : ps[ky * 3 + 1]) * e[1];  // even: Jq/2 = KL+1
+  };
+  struct X2 {
+    Row<T, Q> x;
+    PRow<Q> p;
+    T f[Q];
+  };
+  auto mkx2 = [&](const In2& r, int b) {
+    const bool bin = b >= 1 && b <= Hc - 2;
+    T x[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const T omk = MULTI ? tab[r.p[q] * kTabStride + 9] : om;
+      x[q] = (bin && jin[q]) ? omk * r.f[q] : T(0);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int Jq = J0 + q;
+      if (b & 1) {
+        const T t = term2(r.e[0], r.pe[0], Jq, 2) + term2(r.e[1], r.pe[1], Jq, 0);
+        x[q] += w1 * t;
+      } else {
+        x[q] += w1 * term2(r.e[0], r.pe[0], Jq, 1);
+      }
+    }
+    X2 w;
+    w.x = own_row<T, Q>(x);
+    if constexpr (MULTI) w.p = own_prow<Q>(r.p);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w.f[q] = r.f[q];
+    return w;
+  };
+  // u' row a from x' rows a-1, a, a+1 -> the fine stage's coarse row (e[0] = left lane's last, e[1..Q] own)
+  auto mku2 = [&](const X2& a_, const X2& b_, const X2& c_, int a) {
+    const bool ain = a >= 1 && a <= Hc - 2;
+    T o[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const T acc = kapply<T, Q, MULTI>(a_.x, b_.x, c_.x, a_.p, b_.p, c_.p, q, ks, tab);
+      const T omk = MULTI ? tab[b_.p.a[q + 1] + 9] : om;
+      const T u = omk * (b_.f[q] - acc) + b_.x.a[q + 1];
+      o[q] = (ain && jin[q]) ? u : T(0);
+    }
+    CRow<T, V> c{};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c.e[q + 1] = o[q];
+    c.e[0] = shr1(o[Q - 1], T(0));
+    if constexpr (MULTI) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) c.o[q + 1] = b_.p.a[q + 1];
+      c.o[0] = b_.p.a[0];
+    }
+    return c;
+  };
+
+  // ---- fine stage (level l): k_mg_prolong_zu_ovl ----
+  struct In {
+    T f[V];
+    int p[V];
+  };
+  struct XR {
+    Row<T, V> x;
+    PRow<V> p;
+    T f[V];
+  };
+  auto ld_f = [&](int y) {
+    In r;
+    const long long o = rowo(y);
+    vload<T, V>(fb + o, r.f);
+    if constexpr (MULTI) pload<V>(pb + o, r.p);
+    return r;
+  };
+  auto zero_iterate = [&](const In& r, int y, T (&x)[V]) {
+    const bool rin = y >= 1 && y <= H - 2;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T omk = MULTI ? tab[r.p[k] * kTabStride + 9] : om;
+      x[k] = (rin && cin[k]) ? omk * r.f[k] : T(0);
+    }
+  };
+  auto finish_x = [&](const In& r, const T (&x)[V]) {
+    XR w;
+    w.x = own_row<T, V>(x);
+    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+#pragma unroll
+    for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
+    return w;
+  };
+  auto row_even = [&](const In& r, int y, const CRow<T, V>& ca) {
+    T x[V];
+    zero_iterate(r, y, x);
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] += w1 * crow_term<T, V, MULTI>(ca, k + 1, 1, ps, ptb);
+    return finish_x(r, x);
+  };
+  auto row_odd = [&](const In& r, int y, const CRow<T, V>& ca, const CRow<T, V>& cb) {
+    T x[V];
+    zero_iterate(r, y, x);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T t = crow_term<T, V, MULTI>(ca, k + 1, 2, ps, ptb) + crow_term<T, V, MULTI>(cb, k + 1, 0, ps, ptb);
+      x[k] += w1 * t;
+    }
+    return finish_x(r, x);
+  };
+  auto emit = [&](int y, const XR& a, const XR& b, const XR& c) {
+    T o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const T acc = kapply<T, V, MULTI>(a.x, b.x, c.x, a.p, b.p, c.p, k, ks, tab);
+      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      o[k] = omk * (b.f[k] - acc) + b.x.a[k + 1];
+    }
+    if (own) store_masked<T, V, false>(ob + rowo(y), o, cl, W);
+  };
+
+  // coarse stage start: x' rows a0-1 .. a0+2 -> u' rows a0 (C0), a0+1 (C1)
+  const int a0 = (r0 - 1) / 2;
+  X2 Xa = mkx2(ld2(a0 - 1), a0 - 1);
+  X2 Xb = mkx2(ld2(a0), a0);
+  X2 Xc2 = mkx2(ld2(a0 + 1), a0 + 1);
+  const CRow<T, V> C0 = mku2(Xa, Xb, Xc2, a0);
+  Xa = Xb;
+  Xb = Xc2;
+  Xc2 = mkx2(ld2(a0 + 2), a0 + 2);
+  CRow<T, V> C1 = mku2(Xa, Xb, Xc2, a0 + 1);
+  XR Xp = row_even(ld_f(r0 - 1), r0 - 1, C0);
+  XR Xc = row_odd(ld_f(r0), r0, C0, C1);
+  // iteration y (odd) emits fine rows y, y+1 from fine rows y+1, y+2 and u' row (y+3)/2, which needs x' row
+  // (y+5)/2: those loads are in flight kProlongAhead iterations ahead (ring slots consumed in place)
+  constexpr int D = kProlongAhead;
+  struct Slot {
+    In u1, u2;
+    In2 c;
+  };
+  Slot ring[D];
+  auto fill = [&](Slot& sl, int y) {
+    sl.u1 = ld_f(y + 1);
+    sl.u2 = ld_f(y + 2);
+    sl.c = ld2((y + 5) / 2);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) fill(ring[d], r0 + 2 * d);
+  auto iter = [&](int y, auto slot) {
+    Slot& sl = ring[decltype(slot)::value];
+    const XR Xn = row_even(sl.u1, y + 1, C1);  // row y+1 (even, coarse (y+1)/2 = C1)
+    emit(y, Xp, Xc, Xn);
+    if (y + 1 < r1) {  // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
+      Xa = Xb;
+      Xb = Xc2;
+      Xc2 = mkx2(sl.c, (y + 5) / 2);
+      const CRow<T, V> C2 = mku2(Xa, Xb, Xc2, (y + 3) / 2);
+      const XR Xnn = row_odd(sl.u2, y + 2, C1, C2);
+      emit(y + 1, Xc, Xn, Xnn);
+      Xp = Xn;
+      Xc = Xnn;
+      C1 = C2;
+    }
+    fill(sl, y + 2 * D);
+  };
+  int y = r0;
+  for (; y + 2 * (D - 1) < r1; y += 2 * D) {
+    iter(y, std::integral_constant<int, 0>{});
+    if constexpr (D > 1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 2) iter(y + 4, std::integral_constant<int, 2 % D>{});
+    if constexpr (D > 3) iter(y + 6, std::integral_constant<int, 3 % D>{});
+  }
+  if constexpr (D > 1)
+    if (y < r1) iter(y, std::integral_constant<int, 0>{});
+  if constexpr (D > 2)
+    if (y + 2 < r1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+  if constexpr (D > 3)
+    if (y + 4 < r1) iter(y + 4, std::integral_constant<int, 2 % D>{});
+}
+
+// ---------------------------------------------------------------------------
 // Kernel F: cycle join — the post-smooth of V-cycle k and the pre-smooth + residual + restriction
 // of V-cycle k+1 on one level in ONE pass (temporal blocking across the cycle boundary):
 //   x = u + w1 P(ec)        (FEANet/multigrid.py:177-180, prolongation + correction)
@@ -2776,3 +3057,42 @@ static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const u
   }
 FEA_ZR2_API(f32, float)
 FEA_ZR2_API(f64, double)
+
+template <typename T>
+static int prolong2(const T* fc, const T* ec2, const T* f, T* out, const uint8_t* pid, const uint8_t* pidc,
+                    const uint8_t* pidc2, const T* ktab, const T* omd, int ntab, const T* ptab, int nptab, T w1, int B,
+                    int H, int W, int ld, long long bs, int ldc, long long bsc, int ldc2, long long bsc2,
+                    void* stream) {
+  if (!fc || !ec2 || !f || !out || !ktab || !omd || !ptab || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;
+  if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  if (!coarse_ok<T>(Hc, Wc, ldc2, bsc2)) return FEA_EINVAL;
+  const bool multi = ntab > 1;
+  if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nptab != ntab && nptab != 1)) return FEA_EINVAL;
+  if (multi && (!pid || !pidc || !pidc2 || nptab == 1)) return FEA_EINVAL;
+  MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);
+  g.ec = fc; g.ec2 = ec2; g.f = f; g.out = out; g.pid = pid; g.pidc = pidc; g.pidc2 = pidc2; g.ktab = ktab;
+  g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.w = w1;
+  g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;
+  g.Hc2 = (Hc + 1) / 2; g.Wc2 = (Wc + 1) / 2; g.ldc2 = ldc2; g.bsc2 = bsc2;
+  g.nstrips = div_up(W - 2, Ovl4<T>::S);
+  g.rb = pick_rb(B, g.nstrips, H - 2);
+  g.ntr = div_up(H - 2, g.rb);
+  const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);
+  hipStream_t s = (hipStream_t)stream;
+  if (multi) k_mg_prolong2<T, true><<<grid, 256, 0, s>>>(g);
+  else k_mg_prolong2<T, false><<<grid, 256, 0, s>>>(g);
+  FEA_LAUNCH_CHECK();
+}
+
+#define FEA_PROLONG2_API(SUF, T)                                                                              \
+  extern "C" int fea_mg_prolong2_##SUF(const T* fc, const T* ec2, const T* f, T* out, const uint8_t* pid,      \
+                                       const uint8_t* pidc, const uint8_t* pidc2, const T* ktab, const T* omd,  \
+                                       int ntab, const T* ptab, int nptab, T w1, int B, int H, int W, int ld,   \
+                                       long long bs, int ldc, long long bsc, int ldc2, long long bsc2,          \
+                                       void* stream) {                                                        \
+    return prolong2<T>(fc, ec2, f, out, pid, pidc, pidc2, ktab, omd, ntab, ptab, nptab, w1, B, H, W, ld, bs, ldc, \
+                       bsc, ldc2, bsc2, stream);                                                               \
+  }
+FEA_PROLONG2_API(f32, float)
+FEA_PROLONG2_API(f64, double)

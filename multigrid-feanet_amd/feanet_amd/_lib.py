@@ -45,6 +45,7 @@ _SIGS = {
     "mg_zero_restrict2": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P],
     "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P, P, P, P],
     "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_prolong2": [P, P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P],
     "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, I, LL, I, I, I, I, P],
     "mg_cycle_join": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", "S", I, I, I, I, LL, I, LL, P, P, P, P],

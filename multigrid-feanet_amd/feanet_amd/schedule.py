@@ -195,6 +195,26 @@ def pair_restrictions(steps, can_pair):
     return out
 
 
+def pair_prolongations(steps, can_pair):
+    """Rewrite two consecutive recomputed-iterate prolongations (("prolong_sweep", l+1, OMDF, c, d), then
+    ("prolong_sweep", l, OMDF, d, e)) into one ("prolong_sweep2", l, c, e) step — fea_mg_prolong2, bitwise
+    the two; the intermediate iterate d of level l+1 is then never stored — where can_pair(l) allows it."""
+    out = []
+    i = 0
+    ps = lambda st: st[0] == "prolong_sweep" and st[2] == OMDF
+    while i < len(steps):
+        st = steps[i]
+        if i + 1 < len(steps) and ps(st) and ps(steps[i + 1]):
+            nx = steps[i + 1]
+            if nx[1] == st[1] - 1 and nx[3] == st[4] and can_pair(nx[1]):
+                out.append(("prolong_sweep2", nx[1], st[3], nx[4]))
+                i += 2
+                continue
+        out.append(st)
+        i += 1
+    return out
+
+
 def group_mid(steps, pick_down, pick_up):
     """Rewrite runs of consecutive zero-guess restrictions (("resid_restrict", l, None, None), l
     ascending) and of recomputed prolongations (("prolong_sweep", l, OMDF, csrc, dst), l descending)

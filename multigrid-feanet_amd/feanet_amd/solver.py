@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import OMDF, group_mid, hjac_schedule, pair_restrictions, vcycle_schedule
+from .schedule import OMDF, group_mid, hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
 
 
 _SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
@@ -119,8 +119,8 @@ class MultigridSolver:
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
         mid: run latency-bound coarse levels (B*H*W <= MID_NODES) up to four per launch
             (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels).
-        pair_down: two consecutive zero-guess restrictions left to single-level launches run as one
-            (fea_mg_zero_restrict2, bitwise the two).
+        pair_levels: two consecutive zero-guess restrictions, and two recomputed-iterate prolongations, left
+            to single-level launches run as one each (fea_mg_zero_restrict2 / fea_mg_prolong2, bitwise the two).
     """
 
     MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
@@ -131,7 +131,7 @@ class MultigridSolver:
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_down=True):
+                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_levels=True):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -164,7 +164,7 @@ class MultigridSolver:
         self.zero_start = zero_start
         self.join_cycles = join_cycles
         self.mid = bool(mid)
-        self.pair_down = bool(pair_down)
+        self.pair_levels = bool(pair_levels)
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -370,9 +370,9 @@ class MultigridSolver:
                                          top_zero=self.zero_start)
             if self.mid:
                 steps = group_mid(steps, lambda lv: self._pick_mid(lv, False), lambda lv: self._pick_mid(lv, True))
-            if self.pair_down:
-                steps = pair_restrictions(steps, lambda l: l + 2 < self.L and self.levels[l + 2].H >= 3
-                                          and self.levels[l + 2].W >= 3)
+            if self.pair_levels:
+                ok = lambda l: l + 2 < self.L and self.levels[l + 2].H >= 3 and self.levels[l + 2].W >= 3
+                steps = pair_prolongations(pair_restrictions(steps, ok), ok)
         return [self.bind_step(st) for st in steps], end
 
     def _mid_tile(self, up, a, k):
@@ -457,6 +457,9 @@ class MultigridSolver:
         if kind == "prolong_sweep":
             return ("mg_prolong_sweep", (ptr(l, st[2]), ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l),
                                          pid(l + 1), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l))
+        if kind == "prolong_sweep2":
+            return ("mg_prolong2", (lv[l + 1].f.data_ptr(), ptr(l + 2, st[2]), f, ptr(l, st[3]), pid(l), pid(l + 1),
+                                    pid(l + 2), kt, om, nt, pt, npt, self.w[1]) + geom(l) + cgeom(l) + cgeom(l + 1))
         if kind == "prolong_add":
             return ("mg_prolong_add", (ptr(l, st[2]), ptr(l + 1, st[3]), ptr(l, st[4]), pid(l + 1), pt, npt,
                                        self.w[1]) + geom(l) + cgeom(l))
@@ -939,6 +942,14 @@ class MultigridSolver:
                 n1 = B * (H - 2) * (W - 2)
                 n2 = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
                 total += n0 * (esz + pb) + (n1 + n2) * esz
+                continue
+            if name == "mg_prolong2":  # read f_l, f_{l+1} (+ patterns), e_{l+2}; write u_l
+                B, H, W = args[-9:-6]
+                n0 = B * (H - 2) * (W - 2)
+                H, W = (H + 1) // 2, (W + 1) // 2
+                n1 = B * (H - 2) * (W - 2)
+                n2 = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
+                total += n0 * (2 * esz + pb) + n1 * (esz + pb) + n2 * (esz + pb)
                 continue
             if name == "mg_sweep_restrict":  # (..., B, H, W, ld, bs, ldc, bsc, norm_ws, norm_hist, norm_cnt)
                 B, H, W = args[-10:-7]

@@ -1080,19 +1080,63 @@ def test_zero_restrict2_bitwise(T, problem, n, m, B):
 
 
 def test_solver_pairs_restrictions():
-    """The solver's plan at 4097^2 runs levels 1 and 2 going down as ONE fea_mg_zero_restrict2 launch, and the
-    V-cycle with and without the pairing is bitwise the same."""
+    """The solver's plan at 4097^2 runs levels 1 and 2 as ONE fea_mg_zero_restrict2 launch going down and ONE
+    fea_mg_prolong2 launch going up, and the V-cycle with and without the pairing is bitwise the same."""
     from feanet_amd.solver import MultigridSolver
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
     f = torch.randn(1, 1, 4097, 4097, dtype=torch.float64, device="cuda", generator=g)
     outs = []
     for pair in (True, False):
-        s = MultigridSolver(4096, dtype=torch.float64, pair_down=pair)
+        s = MultigridSolver(4096, dtype=torch.float64, pair_levels=pair)
         names = [nm for nm, _ in s._plan("a")[0]]
-        assert ("mg_zero_restrict2" in names) == pair, names
+        assert ("mg_zero_restrict2" in names) == pair and ("mg_prolong2" in names) == pair, names
         s.set_rhs(f=f)
         s.load()
         s.vcycle(3)
         outs.append(s.solution())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n,m,B", [("poisson", 8, None, 1), ("poisson", 16, None, 3), ("poisson", 64, None, 2),
+                                           ("poisson", 256, None, 1), ("poisson", 512, None, 2),
+                                           ("poisson", 2048, None, 1), ("poisson", 256, 64, 2),
+                                           ("poisson", 64, 512, 1), ("poisson", 488, 120, 1),
+                                           ("interface", 32, None, 3), ("interface", 256, None, 1),
+                                           ("interface", 1024, None, 1)])
+def test_prolong2_bitwise(T, problem, n, m, B):
+    """fea_mg_prolong2 (two recomputed-iterate prolongations + post-sweeps in one pass) is bitwise the two
+    single-level fea_mg_prolong_sweep(u = NULL) launches it replaces, at every size (strip and task edges,
+    rows != columns), batch, dtype, and on the two-material problem with per-pattern learned P; the output's
+    boundary nodes are left untouched."""
+    from feanet_amd import _lib
+    rng = np.random.default_rng(11 * n + B)
+    m_ = n if m is None else m
+    fr = Frame(n, B, T, problem, m=m)
+    c1 = Frame(n // 2, B, T, problem, m=m_ // 2)
+    c2 = Frame(n // 4, B, T, problem, m=m_ // 4)
+    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned=problem == "interface")
+    nt = ktab.shape[0]
+    _, f0 = rand_state(rng, B, (fr.H, fr.W), T)
+    _, f1 = rand_state(rng, B, (c1.H, c1.W), T)
+    e2 = rng.standard_normal((B, c2.H, c2.W)).astype(npdt(T))
+    e2[:, 0, :] = e2[:, -1, :] = e2[:, :, 0] = e2[:, :, -1] = 0
+    fr.put("f", f0)
+    c1.put("f", f1)
+    c2.put("a", e2)
+    c1.put("a", np.zeros((B, c1.H, c1.W)))
+    sent = np.full((B, fr.H, fr.W), 7.0)
+    fr.put("b", sent)
+    _lib.call("mg_prolong_sweep", T, None, c2.L.a.data_ptr(), c1.L.f.data_ptr(), c1.L.a.data_ptr(), c1.pid(), c2.pid(),
+              kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, 0.75, *c1.args(), c2.L.ld, c2.L.bs, None)
+    _lib.call("mg_prolong_sweep", T, None, c1.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), fr.pid(), c1.pid(),
+              kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, 0.75, *fr.args(), c1.L.ld, c1.L.bs, None)
+    ref = fr.get("b")
+    fr.put("b", sent)
+    _lib.call("mg_prolong2", T, c1.L.f.data_ptr(), c2.L.a.data_ptr(), fr.L.f.data_ptr(), fr.L.b.data_ptr(), fr.pid(),
+              c1.pid(), c2.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, 0.75, *fr.args(), c1.L.ld,
+              c1.L.bs, c2.L.ld, c2.L.bs, None)
+    got = fr.get("b")
+    assert np.array_equal(got, ref), f"{np.argwhere(got != ref)[:5]}"
+    assert (got[:, 0, :] == 7).all() and (got[:, :, -1] == 7).all() and (got[:, -1, :] == 7).all()

@@ -34,6 +34,10 @@ def interpret(mg, steps, v, f, compat=None):
             a, k, csrc, dst = st[1:5]
             expanded += [("prolong_sweep", l, "omdf", csrc if l == a + k - 1 else "mid", dst if l == a else "mid")
                          for l in range(a + k - 1, a - 1, -1)]
+        elif st[0] == "resid_restrict2":  # feanet_amd.schedule.pair_restrictions
+            expanded += [("resid_restrict", st[1], None, None), ("resid_restrict", st[1] + 1, None, None)]
+        elif st[0] == "prolong_sweep2":  # feanet_amd.schedule.pair_prolongations
+            expanded += [("prolong_sweep", st[1] + 1, "omdf", st[2], "mid"), ("prolong_sweep", st[1], "omdf", "mid", st[3])]
         else:
             expanded.append(st)
     for st in expanded:
@@ -235,3 +239,31 @@ def test_top_zero_schedule_equals_step_from_zero(problem, nu):
             assert steps[0] == ("resid_restrict", 0, None, None) and steps[-1][2] == "omdf"
         out = interpret(mg, steps, rng.standard_normal(f.shape), f)[0][end]
         np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("groups,npairs", [([], 2), ([(3, 2)], 1), ([(1, 2)], 1), ([(2, 3)], 0)])
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+def test_level_pairing_equals_per_level(problem, groups, npairs):
+    """pair_restrictions / pair_prolongations (fea_mg_zero_restrict2 / fea_mg_prolong2) on the levels the
+    multi-level launches leave: the paired schedule is the per-level one (same V-cycle result with oracle
+    operators), pairs never overlap a multi-level group, and the intermediate iterate of a paired
+    prolongation is never named (it is not stored)."""
+    from feanet_amd.schedule import group_mid, pair_prolongations, pair_restrictions
+    n, L = 64, 6
+    rng = np.random.default_rng(5)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    mg.nu, mg.q2 = (1, 1), False
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    steps, end = vcycle_schedule(L, 1, 1, tail_from=5)
+    pick = lambda levels: [(a, k, 4) for a, k in groups if set(range(a, a + k)) <= set(levels)]
+    ok = lambda l: l + 2 < L
+    paired = pair_prolongations(pair_restrictions(group_mid(steps, pick, pick), ok), ok)
+    kinds = [s[0] for s in paired]
+    assert kinds.count("resid_restrict2") == kinds.count("prolong_sweep2") == npairs
+    for s in paired:
+        if s[0] == "prolong_sweep2":
+            assert s[2] == "a" and s[3] == "a"
+    ref = interpret(mg, steps, v, f)[0][end]
+    out = interpret(mg, paired, v, f)[0][end]
+    np.testing.assert_array_equal(out, ref)

@@ -2,7 +2,7 @@
 # solver, then the metric cycle's kernel times under a trace
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}; export TMPDIR=/tmp; T=gpurun_out/r03q; mkdir -p $T
-timeout -k 10 300 python -u -m pytest tests/test_gpu_mg.py -m gpu -x -q --timeout 120 --timeout-method thread -k "zero_restrict2 or pairs_restrictions" > $T/pytest_zr2.log 2>&1 || { echo "zr2 tests failed"; tail -40 $T/pytest_zr2.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_mg.py -m gpu -x -q --timeout 120 --timeout-method thread -k "zero_restrict2 or prolong2 or pairs_restrictions" > $T/pytest_zr2.log 2>&1 || { echo "zr2 tests failed"; tail -40 $T/pytest_zr2.log; exit 1; }
 tail -2 $T/pytest_zr2.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_mg.py tests/test_gpu_configs.py tests/test_gpu_mid.py tests/test_gpu_dd.py -m gpu -x -q --timeout 300 --timeout-method thread > $T/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $T/pytest.log; exit 1; }
 tail -2 $T/pytest.log

@@ -14,7 +14,7 @@ from feanet_amd import _lib  # noqa: E402
 from feanet_amd.solver import MultigridSolver  # noqa: E402
 
 for n, B, T in ((4096, 1, torch.float64), (8192, 1, torch.float64), (1024, 64, torch.float32)):
-    s = MultigridSolver(n, dtype=T, batch=B, pair_down=False)
+    s = MultigridSolver(n, dtype=T, batch=B, pair_levels=False)
     lv = s.levels
     g = torch.Generator(device="cuda")
     g.manual_seed(1)
