@@ -36,7 +36,7 @@ smallest depths for which the validity simulation keeps every owned node exact.
 import torch
 
 from . import _lib
-from .schedule import vcycle_schedule
+from .schedule import pair_prolongations, pair_restrictions, vcycle_schedule
 from .solver import MultigridSolver
 
 
@@ -491,6 +491,11 @@ class DDSolver:
         segs = []
         fold = self.comm is not None and hasattr(self.comm, "halo_pack")
         place = None  # the gathered blocks' placement, folded into the next kernel segment
+        if self.local.pair_levels:
+            # two-level launches on the distributed levels between the communication steps (same per-level
+            # computations on the same local nodes, so the ghost validity of every step is unchanged)
+            ok = lambda l: l >= 1 and l + 2 <= self.Ld
+            steps = pair_prolongations(pair_restrictions(steps, ok), ok)
         for st in steps:
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
                 if self.P == 1:
