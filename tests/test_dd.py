@@ -103,8 +103,10 @@ def test_default_agglomeration():
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_c4_agglomeration_level_is_the_measured_best(P):
     """C4 (8193^2 over the bench's 2x1 / 2x2 / 4x2 blocks): the default agglomeration level is the one the
-    per-rank projection measured fastest — Ld = 4 (the 513^2 level) at every rank count, against Ld = 3, 5, 6
-    (tools/dd_projection.py, profiles/r03_dd/dd_projection.txt: 8 ranks 151.8 us vs 158.5 / 155.9 / 154.7)."""
+    per-rank projection chose — Ld = 4 (the 513^2 level): fastest at every rank count against Ld = 3, 5, 6
+    (tools/dd_projection.py, profiles/r03_dd/dd_projection.txt: 8 ranks 151.8 us vs 158.5 / 155.9 / 154.7), and
+    with the round-3 two-level launches within the run-to-run spread of Ld = 3 / 5 at 4 and 8 ranks
+    (profiles/r03_dd/dd_projection_paired.txt: 134.0 vs 135.8 / 135.7 us at 8 ranks)."""
     from feanet_amd.dd import default_grid
     Pr, Pc = default_grid(P)
     assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == 4
