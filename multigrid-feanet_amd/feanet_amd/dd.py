@@ -372,13 +372,16 @@ class DDSolver:
     LocalGroup; agglomerate: Ld (default: see default_agglomeration); overlap_l0: send the finest level's halo
     as a second message batch that completes only before the next level-0 kernel (overlapping levels 1 .. and
     the coarse solve) instead of with the coarse-level halo in one batch — one more message group and one
-    more unpack launch per cycle; other args as MultigridSolver (Poisson).
+    more unpack launch per cycle; graph_min: kernel segments of fewer launches run eagerly instead of as HIP
+    graphs (on this chip a graph launch between two communication steps costs ~8 us of GPU time, a short
+    eager segment less); other args as MultigridSolver (Poisson).
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
-                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False):
+                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
+        self.graph_min = graph_min
         self.rank, self.P = rank, world
         self.Pr, self.Pc = grid if grid is not None else (world, 1)
         self.ri, self.ci = divmod(rank, self.Pc)
@@ -591,6 +594,9 @@ class DDSolver:
         launches = segs[i][1]
         gkey = (key, i)
         stream = torch.cuda.current_stream(self.device)
+        if len(launches) < self.graph_min:  # a graph launch costs more GPU time than a few eager launches
+            _launch_list(launches, self.dtype, stream)
+            return
         if not self.use_graph or gkey not in self._graphs:
             if self.use_graph:
                 self._graphs[gkey] = None  # eager once, capture on the second use

@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--ld", default=None, help="agglomeration levels to try (default: default-1 .. default+2)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-pack", action="store_true", help="leave out the halo pack / unpack kernels")
+    ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly (no HIP graphs)")
+    ap.add_argument("--graph-min", type=int, default=None, help="DDSolver(graph_min=): shorter segments eager")
     args = ap.parse_args()
     n = args.n
     g = torch.Generator(device="cuda")
@@ -133,7 +135,9 @@ def main():
         rec["ranks"][P] = {"grid": f"{Pr}x{Pc}", "rank": r, "default_ld": d, "ld": {}}
         for Ld in lds:
             try:
-                s = DDSolver(n, n, r, P, comm=NullComm() if args.no_pack else PackComm(), agglomerate=Ld, grid=(Pr, Pc))
+                s = DDSolver(n, n, r, P, comm=NullComm() if args.no_pack else PackComm(), agglomerate=Ld, grid=(Pr, Pc),
+                             graph=not args.no_graph,
+                             **({} if args.graph_min is None else {"graph_min": args.graph_min}))
             except ValueError as e:
                 print(f"P={P} {Pr}x{Pc} Ld={Ld}: not partitionable ({e})", flush=True)
                 continue
