@@ -273,6 +273,37 @@ def single_gpu_same_grid(m, n, T, B, steps, ms_dd):
             "workload": f"{m + 1}x{n + 1} poisson V-cycle on one GPU (MultigridSolver, no decomposition), rank 0"}
 
 
+def dd_parity_check(s, m, n, T, B, ws, cycles=3):
+    """Every rank: the decomposed solver's owned block after `cycles` V-cycles from zero against the single-GPU
+    MultigridSolver's on the same global grid and seeded rhs (run on the rank's own GPU).  The decomposed
+    cycle is bitwise the single-GPU one by construction (tests/test_gpu_dd.py); this puts that claim on the
+    line of every multi-GPU run, i.e. on the RCCL path itself.  Returns the max over ranks of the largest
+    absolute difference and of the count of differing nodes."""
+    from feanet_amd.solver import MultigridSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    f = torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g)
+    s.load()
+    s.vcycle(cycles)
+    (y0, y1), (x0, x1), u = s.owned_block()
+    ref = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B)
+    ref.set_rhs(f=f)
+    del f
+    ref.load()
+    ref.vcycle(cycles)
+    exp = ref.solution()[:, :, y0:y1, x0:x1]
+    diff = (u - exp).abs()
+    out = torch.tensor([diff.max().item(), float((u != exp).sum().item())], dtype=torch.float64, device="cuda")
+    del ref, exp, diff, u
+    torch.cuda.empty_cache()
+    if ws > 1:
+        torch.distributed.all_reduce(out, op=torch.distributed.ReduceOp.MAX)
+    return {"cycles": cycles, "bitwise_equal": bool(out[1].item() == 0), "max_abs_diff": out[0].item(),
+            "max_differing_nodes_per_rank": int(out[1].item()),
+            "against": f"single-GPU MultigridSolver on the same {m + 1}x{n + 1} grid, V-cycles from zero, every "
+                       f"rank's owned block"}
+
+
 def dd_domain(P, n0):
     """Weak-scaled global grid for P slabs of n0 x n0 intervals each, aspect ratio <= 2 when P is a
     power of two: 1 -> n0 x n0, 2 -> 2n0 x n0, 4 -> 2n0 x 2n0, 8 -> 4n0 x 2n0 (rows x columns)."""
@@ -466,6 +497,8 @@ def main():
         if rank == 0:
             rec["single_gpu_same_grid"] = single_gpu_same_grid(m, nc, T, B, args.steps, ms_step)
         barrier(ws)
+    if mode == "dd":
+        rec["dd_parity"] = dd_parity_check(s, m, nc, T, B, ws)
     if rank == 0 and ws == 1 and mode == "single" and not args.no_cpu_baseline and args.problem == "poisson" \
             and B == 1:
         log("[bench] timing the CPU oracle baseline ...")

@@ -1,0 +1,42 @@
+"""The multi-GPU bench line end to end: bench.py under torch.distributed.run with two ranks on the one GPU
+(gloo, device halos staged through the host), as the driver's N > 1 runs launch it (they use RCCL, one GPU
+per rank).  The line must carry its strong-scaling base point and a dd_parity record in which every rank's
+owned block equals the single-GPU solver's bitwise."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    p = sk.getsockname()[1]
+    sk.close()
+    return p
+
+
+@pytest.mark.parametrize("ranks,grid", [(2, None), (4, "2x2")])
+def test_bench_dd_line_parity(ranks, grid):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(ranks), "--steps", "3", "--warmup", "1", "--backend", "gloo", "--global-n", "1024",
+           "--kernel-reps", "2"] + (["--grid", grid] if grid else [])
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == ranks and rec["scaling"] == "strong" and rec["config"]["mode"] == "dd"
+    par = rec["dd_parity"]
+    assert par["bitwise_equal"] and par["max_abs_diff"] == 0.0, par
+    base = rec["single_gpu_same_grid"]
+    assert base["ms_per_step"] > 0 and base["workload"].startswith("1025x1025")
