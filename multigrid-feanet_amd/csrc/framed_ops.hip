@@ -36,6 +36,15 @@ struct Frame {
 constexpr int kRB = 32;     // fine rows per task (even: tasks start on odd rows)
 constexpr int kWaves = 4;   // waves (tasks) per block
 constexpr int kTabStride = 10;  // LDS table row: 9 stencil weights + omega/d
+// Pattern windows (PRow, CRow::o, the prolongation's pe) hold BYTE offsets of a pattern's LDS table row
+// (pattern * kTabStride * sizeof(T)), so a table read is one ds_read at that address
+// plus the tap as an immediate offset, with no per-read index scaling
+template <typename T>
+__host__ __device__ constexpr int tab_row_bytes() { return kTabStride * (int)sizeof(T); }
+template <typename T>
+__device__ __forceinline__ T tabv(const T* t, int off, int d) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(t) + off + d * (int)sizeof(T));
+}
 // The restricted field f_c (a quarter of the level's bytes) is stored with normal stores even when
 // the level's own stores stream past the caches: the next kernel (the coarse level's restriction)
 // reads it straight back, from the Infinity Cache instead of HBM.
@@ -138,7 +147,7 @@ struct Row {
   T a[V + 3];
 };
 template <int V>
-struct PRow {  // LDS table offsets (pattern * kTabStride) for the same columns
+struct PRow {  // LDS table row byte offsets (pattern * tab_row_bytes<T>()) for the same columns
   int a[V + 3];
 };
 
@@ -186,14 +195,14 @@ __device__ __forceinline__ RawP<V> raw_prow(const uint8_t* __restrict__ pp, int 
   return r;
 }
 
-template <int V>
-__device__ __forceinline__ PRow<V> finish(const RawP<V>& r) {
+template <typename T, int V>
+__device__ __forceinline__ PRow<V> finish_p(const RawP<V>& r) {
   PRow<V> w;
 #pragma unroll
-  for (int k = 0; k < V; ++k) w.a[k + 1] = r.x[k] * kTabStride;
-  w.a[0] = shr1(r.x[V - 1], r.h[V - 1]) * kTabStride;
-  w.a[V + 1] = shl1(r.x[0], r.h[0]) * kTabStride;
-  w.a[V + 2] = shl1(r.x[1 % V], r.h[1 % V]) * kTabStride;
+  for (int k = 0; k < V; ++k) w.a[k + 1] = r.x[k] * tab_row_bytes<T>();
+  w.a[0] = shr1(r.x[V - 1], r.h[V - 1]) * tab_row_bytes<T>();
+  w.a[V + 1] = shl1(r.x[0], r.h[0]) * tab_row_bytes<T>();
+  w.a[V + 2] = shl1(r.x[1 % V], r.h[1 % V]) * tab_row_bytes<T>();
   return w;
 }
 
@@ -214,15 +223,15 @@ __device__ __forceinline__ T kapply(const Row<T, V>& w0, const Row<T, V>& w1, co
     acc += ks[7] * w2.a[k + 1];
     acc += ks[8] * w2.a[k + 2];
   } else {
-    acc = tab[p0.a[k] + 0] * w0.a[k];
-    acc += tab[p0.a[k + 1] + 1] * w0.a[k + 1];
-    acc += tab[p0.a[k + 2] + 2] * w0.a[k + 2];
-    acc += tab[p1.a[k] + 3] * w1.a[k];
-    acc += tab[p1.a[k + 1] + 4] * w1.a[k + 1];
-    acc += tab[p1.a[k + 2] + 5] * w1.a[k + 2];
-    acc += tab[p2.a[k] + 6] * w2.a[k];
-    acc += tab[p2.a[k + 1] + 7] * w2.a[k + 1];
-    acc += tab[p2.a[k + 2] + 8] * w2.a[k + 2];
+    acc = tabv(tab, p0.a[k], 0) * w0.a[k];
+    acc += tabv(tab, p0.a[k + 1], 1) * w0.a[k + 1];
+    acc += tabv(tab, p0.a[k + 2], 2) * w0.a[k + 2];
+    acc += tabv(tab, p1.a[k], 3) * w1.a[k];
+    acc += tabv(tab, p1.a[k + 1], 4) * w1.a[k + 1];
+    acc += tabv(tab, p1.a[k + 2], 5) * w1.a[k + 2];
+    acc += tabv(tab, p2.a[k], 6) * w2.a[k];
+    acc += tabv(tab, p2.a[k + 1], 7) * w2.a[k + 1];
+    acc += tabv(tab, p2.a[k + 2], 8) * w2.a[k + 2];
   }
   return acc;
 }
@@ -419,8 +428,8 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
     PRow<V> p0{}, p1{}, p2{};
     RawP<V> px{};
     if constexpr (MULTI) {
-      p0 = finish(raw_prow<V>(pb + rowo(r0 - 1), lane));
-      p1 = finish(raw_prow<V>(pb + rowo(r0), lane));
+      p0 = finish_p<T>(raw_prow<V>(pb + rowo(r0 - 1), lane));
+      p1 = finish_p<T>(raw_prow<V>(pb + rowo(r0), lane));
       px = raw_prow<V>(pb + rowo(r0 + 1), lane);
     }
     for (int r = r0; r < r1; ++r) {
@@ -431,12 +440,12 @@ __global__ __launch_bounds__(256) void k_mg_sweep(MgArgs<T> g) {
       RawP<V> pn{};
       if constexpr (MULTI) pn = raw_prow<V>(pb + rowo(r + 2), lane);
       const Row<T, V> w2 = finish(nx);
-      if constexpr (MULTI) p2 = finish(px);
+      if constexpr (MULTI) p2 = finish_p<T>(px);
       T o[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const T acc = kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
-        const T omk = MULTI ? tab[p1.a[k + 1] + 9] : om;
+        const T omk = MULTI ? tabv(tab, p1.a[k + 1], 9) : om;
         o[k] = omk * (fx[k] - acc) + w1.a[k + 1];
       }
       store_masked<T, V, NT>(ob + rowo(r) + V * lane, o, cl, W);
@@ -550,13 +559,13 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
   };
   auto fin_w = [&](const RawW& r, int y) {
     WRow w;
-    if constexpr (MULTI) w.p = finish(r.p);
+    if constexpr (MULTI) w.p = finish_p<T>(r.p);
     w.f = finish(r.f);
     if constexpr (ZERO) {
       const bool rin = y >= 1 && y <= H - 2;
 #pragma unroll
       for (int j = 0; j < V + 3; ++j) {
-        const T omj = MULTI ? tab[w.p.a[j] + 9] : om;
+        const T omj = MULTI ? tabv(tab, w.p.a[j], 9) : om;
         w.u.a[j] = (rin && cin[j]) ? omj * w.f.a[j] : T(0);
       }
     } else {
@@ -633,15 +642,15 @@ __global__ __launch_bounds__(256) void k_mg_resid_restrict(MgArgs<T> g) {
         acc += rs[7] * Rc[2 * q + 1];
         acc += rs[8] * Rc[2 * q + 2];
       } else {
-        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
-        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
-        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
-        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
-        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
-        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
-        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
-        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
-        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+        acc = tabv(rtb, Pa.a[2 * q + 1], 0) * Ra[2 * q];
+        acc += tabv(rtb, Pa.a[2 * q + 2], 1) * Ra[2 * q + 1];
+        acc += tabv(rtb, Pa.a[2 * q + 3], 2) * Ra[2 * q + 2];
+        acc += tabv(rtb, Pb.a[2 * q + 1], 3) * Rb[2 * q];
+        acc += tabv(rtb, Pb.a[2 * q + 2], 4) * Rb[2 * q + 1];
+        acc += tabv(rtb, Pb.a[2 * q + 3], 5) * Rb[2 * q + 2];
+        acc += tabv(rtb, Pc.a[2 * q + 1], 6) * Rc[2 * q];
+        acc += tabv(rtb, Pc.a[2 * q + 2], 7) * Rc[2 * q + 1];
+        acc += tabv(rtb, Pc.a[2 * q + 3], 8) * Rc[2 * q + 2];
       }
       o[q] = w0 * acc;
     }
@@ -697,13 +706,13 @@ __device__ __forceinline__ Row<T, V> own_row(const T (&x)[V]) {  // window L, ow
   w.a[V + 1] = shl1(x[0], T(0));
   return w;
 }
-template <int V>
+template <typename T, int V>
 __device__ __forceinline__ PRow<V> own_prow(const int (&x)[V]) {
   PRow<V> w;
 #pragma unroll
-  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * kTabStride;
-  w.a[0] = shr1(x[V - 1], 0) * kTabStride;
-  w.a[V + 1] = shl1(x[0], 0) * kTabStride;
+  for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * tab_row_bytes<T>();
+  w.a[0] = shr1(x[V - 1], 0) * tab_row_bytes<T>();
+  w.a[V + 1] = shl1(x[0], 0) * tab_row_bytes<T>();
   return w;
 }
 
@@ -774,7 +783,7 @@ __device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const Ta
     w.u = own_row<T, V>(r.u);
 #pragma unroll
     for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
-    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
     return w;
   };
   auto owns = [&](int y) { return own && y >= 2 * I0 - 1 && (y < 2 * I1 - 1 || I1 == Hc - 1) && y <= H - 2; };
@@ -785,7 +794,7 @@ __device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const Ta
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acc = kapply<T, V, MULTI>(a.u, b.u, c.u, a.p, b.p, c.p, k, ks, tab);
-      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      const T omk = MULTI ? tabv(tab, b.p.a[k + 1], 9) : om;
       const T rr = b.f[k] - acc;
       const T v = omk * rr + b.u.a[k + 1];
       o[k] = (rin && cin[k]) ? v : b.u.a[k + 1];
@@ -811,9 +820,9 @@ __device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const Ta
         t += rs[ky * 3 + 1] * r[2 * q + 1];
         t += rs[ky * 3 + 2] * r[2 * q + 2];
       } else {
-        t = rtb[sy.p.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
-        t += rtb[sy.p.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
-        t += rtb[sy.p.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
+        t = tabv(rtb, sy.p.a[2 * q + 1], ky * 3 + 0) * r[2 * q];
+        t += tabv(rtb, sy.p.a[2 * q + 2], ky * 3 + 1) * r[2 * q + 1];
+        t += tabv(rtb, sy.p.a[2 * q + 3], ky * 3 + 2) * r[2 * q + 2];
       }
       acc[q] = init ? t : acc[q] + t;
     }
@@ -969,7 +978,7 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
       w.f[k] = r.f[k];
     }
     w.v = own_row<T, V>(x);
-    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
     return w;
   };
   auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
@@ -1021,15 +1030,15 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
         acc += rs[7] * Rc[2 * q + 1];
         acc += rs[8] * Rc[2 * q + 2];
       } else {
-        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
-        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
-        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
-        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
-        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
-        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
-        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
-        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
-        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+        acc = tabv(rtb, Pa.a[2 * q + 1], 0) * Ra[2 * q];
+        acc += tabv(rtb, Pa.a[2 * q + 2], 1) * Ra[2 * q + 1];
+        acc += tabv(rtb, Pa.a[2 * q + 3], 2) * Ra[2 * q + 2];
+        acc += tabv(rtb, Pb.a[2 * q + 1], 3) * Rb[2 * q];
+        acc += tabv(rtb, Pb.a[2 * q + 2], 4) * Rb[2 * q + 1];
+        acc += tabv(rtb, Pb.a[2 * q + 3], 5) * Rb[2 * q + 2];
+        acc += tabv(rtb, Pc.a[2 * q + 1], 6) * Rc[2 * q];
+        acc += tabv(rtb, Pc.a[2 * q + 2], 7) * Rc[2 * q + 1];
+        acc += tabv(rtb, Pc.a[2 * q + 3], 8) * Rc[2 * q + 2];
       }
       o[q] = w0 * acc;
     }
@@ -1162,7 +1171,7 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
       w.f[k] = r.f[k];
     }
     w.v = own_row<T, V>(x);
-    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
     return w;
   };
   auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
@@ -1204,7 +1213,7 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
     if constexpr (MULTI) {
       Qa = Qb;
       Qb = Qc;
-      Qc = own_prow<Q>(pq);
+      Qc = own_prow<T, Q>(pq);
     }
     if (n >= 2) {
       // residual row I-1 of level l+1 (k_mg_zero_restrict's resid on the coarse values)
@@ -1233,15 +1242,15 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
             acc += rs[7] * R.a[B0 + 1];
             acc += rs[8] * R.a[B0 + 2];
           } else {
-            acc = rtb[So.a[B0] + 0] * Ro.a[B0];
-            acc += rtb[So.a[B0 + 1] + 1] * Ro.a[B0 + 1];
-            acc += rtb[So.a[B0 + 2] + 2] * Ro.a[B0 + 2];
-            acc += rtb[Se.a[B0] + 3] * Re.a[B0];
-            acc += rtb[Se.a[B0 + 1] + 4] * Re.a[B0 + 1];
-            acc += rtb[Se.a[B0 + 2] + 5] * Re.a[B0 + 2];
-            acc += rtb[Qb.a[B0] + 6] * R.a[B0];
-            acc += rtb[Qb.a[B0 + 1] + 7] * R.a[B0 + 1];
-            acc += rtb[Qb.a[B0 + 2] + 8] * R.a[B0 + 2];
+            acc = tabv(rtb, So.a[B0], 0) * Ro.a[B0];
+            acc += tabv(rtb, So.a[B0 + 1], 1) * Ro.a[B0 + 1];
+            acc += tabv(rtb, So.a[B0 + 2], 2) * Ro.a[B0 + 2];
+            acc += tabv(rtb, Se.a[B0], 3) * Re.a[B0];
+            acc += tabv(rtb, Se.a[B0 + 1], 4) * Re.a[B0 + 1];
+            acc += tabv(rtb, Se.a[B0 + 2], 5) * Re.a[B0 + 2];
+            acc += tabv(rtb, Qb.a[B0], 6) * R.a[B0];
+            acc += tabv(rtb, Qb.a[B0 + 1], 7) * R.a[B0 + 1];
+            acc += tabv(rtb, Qb.a[B0 + 2], 8) * R.a[B0 + 2];
           }
           if (!(Jm & 1) && M >= Mlo && M < Mhi && M <= Wc2 - 2) cb2[(long long)(K + 1) * g.ldc2 + M] = w0 * acc;
         }
@@ -1301,15 +1310,15 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
         acc += rs[7] * Rc[2 * q + 1];
         acc += rs[8] * Rc[2 * q + 2];
       } else {
-        acc = rtb[Pa.a[2 * q + 1] + 0] * Ra[2 * q];
-        acc += rtb[Pa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
-        acc += rtb[Pa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
-        acc += rtb[Pb.a[2 * q + 1] + 3] * Rb[2 * q];
-        acc += rtb[Pb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
-        acc += rtb[Pb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
-        acc += rtb[Pc.a[2 * q + 1] + 6] * Rc[2 * q];
-        acc += rtb[Pc.a[2 * q + 2] + 7] * Rc[2 * q + 1];
-        acc += rtb[Pc.a[2 * q + 3] + 8] * Rc[2 * q + 2];
+        acc = tabv(rtb, Pa.a[2 * q + 1], 0) * Ra[2 * q];
+        acc += tabv(rtb, Pa.a[2 * q + 2], 1) * Ra[2 * q + 1];
+        acc += tabv(rtb, Pa.a[2 * q + 3], 2) * Ra[2 * q + 2];
+        acc += tabv(rtb, Pb.a[2 * q + 1], 3) * Rb[2 * q];
+        acc += tabv(rtb, Pb.a[2 * q + 2], 4) * Rb[2 * q + 1];
+        acc += tabv(rtb, Pb.a[2 * q + 3], 5) * Rb[2 * q + 2];
+        acc += tabv(rtb, Pc.a[2 * q + 1], 6) * Rc[2 * q];
+        acc += tabv(rtb, Pc.a[2 * q + 2], 7) * Rc[2 * q + 1];
+        acc += tabv(rtb, Pc.a[2 * q + 3], 8) * Rc[2 * q + 2];
       }
       o[q] = w0 * acc;
     }
@@ -1385,9 +1394,9 @@ __device__ __forceinline__ CRow<T, V> finish_c(const RawC<T, V>& r) {
   c.e[Q + 1] = shl1(r.x[0], r.h);
   if constexpr (MULTI) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q) c.o[q + 1] = r.px[q] * kTabStride;
-    c.o[0] = shr1(r.px[Q - 1], r.ph) * kTabStride;
-    c.o[Q + 1] = shl1(r.px[0], r.ph) * kTabStride;
+    for (int q = 0; q < Q; ++q) c.o[q + 1] = r.px[q] * tab_row_bytes<T>();
+    c.o[0] = shr1(r.px[Q - 1], r.ph) * tab_row_bytes<T>();
+    c.o[Q + 1] = shl1(r.px[0], r.ph) * tab_row_bytes<T>();
   }
   return c;
 }
@@ -1398,11 +1407,11 @@ __device__ __forceinline__ T crow_term(const CRow<T, V>& c, int j, int ky, const
   const int k = j - 1;
   if ((k & 1) != 0) {  // even fine column: one coarse node, kx = 1
     const int i = (k + 1) / 2;
-    return (MULTI ? ptb[c.o[i] + ky * 3 + 1] : ps[ky * 3 + 1]) * c.e[i];
+    return (MULTI ? tabv(ptb, c.o[i], ky * 3 + 1) : ps[ky * 3 + 1]) * c.e[i];
   } else {  // odd fine column: coarse nodes k/2 (kx = 2) and k/2+1 (kx = 0)
     const int i = k / 2;
-    T t = (MULTI ? ptb[c.o[i] + ky * 3 + 2] : ps[ky * 3 + 2]) * c.e[i];
-    t += (MULTI ? ptb[c.o[i + 1] + ky * 3 + 0] : ps[ky * 3 + 0]) * c.e[i + 1];
+    T t = (MULTI ? tabv(ptb, c.o[i], ky * 3 + 2) : ps[ky * 3 + 2]) * c.e[i];
+    t += (MULTI ? tabv(ptb, c.o[i + 1], ky * 3 + 0) : ps[ky * 3 + 0]) * c.e[i + 1];
     return t;
   }
 }
@@ -1492,7 +1501,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
   };
   auto fp = [&](const RawP<V>& r) {
     PRow<V> p{};
-    if constexpr (MULTI && SWEEP) p = finish(r);
+    if constexpr (MULTI && SWEEP) p = finish_p<T>(r);
     return p;
   };
   auto rf = [&](int y, T (&fv)[V]) {
@@ -1507,7 +1516,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
       for (int k = 0; k < V; ++k) fo[k] = r.a[k + 1];
 #pragma unroll
       for (int j = 0; j < V + 3; ++j) {
-        const T omj = MULTI ? tab[p.a[j] + 9] : om;
+        const T omj = MULTI ? tabv(tab, p.a[j], 9) : om;
         r.a[j] = (rin && cin[j]) ? omj * r.a[j] : T(0);
       }
     }
@@ -1520,7 +1529,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong(MgArgs<T> g) {
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const T acc = kapply<T, V, MULTI>(a, b, c, pa, pbb, pc, k, ks, tab);
-        const T omk = MULTI ? tab[pbb.a[k + 1] + 9] : om;
+        const T omk = MULTI ? tabv(tab, pbb.a[k + 1], 9) : om;
         o[k] = omk * (fv[k] - acc) + b.a[k + 1];
       }
     } else {
@@ -1708,8 +1717,8 @@ __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
     c.e[0] = shr1(r.x[Q - 1], T(0));
     if constexpr (MULTI) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * kTabStride;
-      c.o[0] = shr1(r.p[Q - 1], 0) * kTabStride;
+      for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * tab_row_bytes<T>();
+      c.o[0] = shr1(r.p[Q - 1], 0) * tab_row_bytes<T>();
     }
     return c;
   };
@@ -1725,7 +1734,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
   auto finish_x = [&](const In& r, const T (&x)[V]) {
     XR w;
     w.x = own_row<T, V>(x);
-    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
 #pragma unroll
     for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
     return w;
@@ -1752,7 +1761,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acc = kapply<T, V, MULTI>(a.x, b.x, c.x, a.p, b.p, c.p, k, ks, tab);
-      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      const T omk = MULTI ? tabv(tab, b.p.a[k + 1], 9) : om;
       o[k] = omk * (b.f[k] - acc) + b.x.a[k + 1];
     }
     if (own) store_masked<T, V, NT>(ob + rowo(y), o, cl, W);
@@ -1899,8 +1908,8 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
       r.e[h][0] = e3b[o];
       r.e[h][1] = e3b[o + 1];
       if constexpr (MULTI) {
-        r.pe[h][0] = p3b[o] * kTabStride;
-        r.pe[h][1] = p3b[o + 1] * kTabStride;
+        r.pe[h][0] = p3b[o] * tab_row_bytes<T>();
+        r.pe[h][1] = p3b[o + 1] * tab_row_bytes<T>();
       }
     }
     return r;
@@ -1908,11 +1917,11 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
   // crow_term on level l+2 values for coarse column Jq (bitwise k_mg_prolong_zu_ovl's coarse term)
   auto term2 = [&](const T (&e)[2], const int (&pe)[2], int Jq, int ky) -> T {
     if (Jq & 1) {  // odd: (Jq-1)/2 (kx = 2) and (Jq+1)/2 (kx = 0) — KL and KL+1
-      T t = (MULTI ? ptb[pe[0] + ky * 3 + 2] : ps[ky * 3 + 2]) * e[0];
-      t += (MULTI ? ptb[pe[1] + ky * 3 + 0] : ps[ky * 3 + 0]) * e[1];
+      T t = (MULTI ? tabv(ptb, pe[0], ky * 3 + 2) : ps[ky * 3 + 2]) * e[0];
+      t += (MULTI ? tabv(ptb, pe[1], ky * 3 + 0) : ps[ky * 3 + 0]) * e[1];
       return t;
     }
-    return (MULTI ? ptb[pe[1] + ky * 3 + 1] : ps[ky * 3 + 1]) * e[1];  // even: Jq/2 = KL+1
+    return (MULTI ? tabv(ptb, pe[1], ky * 3 + 1) : ps[ky * 3 + 1]) * e[1];  // even: Jq/2 = KL+1
   };
   struct X2 {
     Row<T, Q> x;
@@ -1939,7 +1948,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
     }
     X2 w;
     w.x = own_row<T, Q>(x);
-    if constexpr (MULTI) w.p = own_prow<Q>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, Q>(r.p);
 #pragma unroll
     for (int q = 0; q < Q; ++q) w.f[q] = r.f[q];
     return w;
@@ -1951,7 +1960,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const T acc = kapply<T, Q, MULTI>(a_.x, b_.x, c_.x, a_.p, b_.p, c_.p, q, ks, tab);
-      const T omk = MULTI ? tab[b_.p.a[q + 1] + 9] : om;
+      const T omk = MULTI ? tabv(tab, b_.p.a[q + 1], 9) : om;
       const T u = omk * (b_.f[q] - acc) + b_.x.a[q + 1];
       o[q] = (ain && jin[q]) ? u : T(0);
     }
@@ -1995,7 +2004,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
   auto finish_x = [&](const In& r, const T (&x)[V]) {
     XR w;
     w.x = own_row<T, V>(x);
-    if constexpr (MULTI) w.p = own_prow<V>(r.p);
+    if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
 #pragma unroll
     for (int k = 0; k < V; ++k) w.f[k] = r.f[k];
     return w;
@@ -2022,7 +2031,7 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acc = kapply<T, V, MULTI>(a.x, b.x, c.x, a.p, b.p, c.p, k, ks, tab);
-      const T omk = MULTI ? tab[b.p.a[k + 1] + 9] : om;
+      const T omk = MULTI ? tabv(tab, b.p.a[k + 1], 9) : om;
       o[k] = omk * (b.f[k] - acc) + b.x.a[k + 1];
     }
     if (own) store_masked<T, V, false>(ob + rowo(y), o, cl, W);
@@ -2261,7 +2270,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acck = kapply<T, V, MULTI>(a, b, c, pa, pb_, pc, k, ks, tab);
-      const T omk = MULTI ? tab[pb_.a[k + 1] + 9] : om;
+      const T omk = MULTI ? tabv(tab, pb_.a[k + 1], 9) : om;
       const T rr = fy[k] - acck;
       const T v = omk * rr + b.a[k + 1];
       o[k] = (rin && cin[k]) ? v : keep[k];
@@ -2322,7 +2331,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
     P3 = P2;
     P2 = P1;
     P1 = P0;
-    if constexpr (MULTI) P0 = own_prow<V>(p0);
+    if constexpr (MULTI) P0 = own_prow<T, V>(p0);
     // 2. v(y-s) = J(x) (boundary nodes keep u)
     if (n >= 2) {
       T v[V];
@@ -2358,9 +2367,9 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
               t += rs[ky * 3 + 1] * r[2 * q + 1];
               t += rs[ky * 3 + 2] * r[2 * q + 2];
             } else {
-              t = rtb[P3.a[2 * q + 1] + ky * 3 + 0] * r[2 * q];
-              t += rtb[P3.a[2 * q + 2] + ky * 3 + 1] * r[2 * q + 1];
-              t += rtb[P3.a[2 * q + 3] + ky * 3 + 2] * r[2 * q + 2];
+              t = tabv(rtb, P3.a[2 * q + 1], ky * 3 + 0) * r[2 * q];
+              t += tabv(rtb, P3.a[2 * q + 2], ky * 3 + 1) * r[2 * q + 1];
+              t += tabv(rtb, P3.a[2 * q + 3], ky * 3 + 2) * r[2 * q + 2];
             }
             return t;
           };
@@ -2507,8 +2516,8 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
   PRow<V> p0{}, p1{}, p2{};
   RawP<V> px{};
   if constexpr (MULTI) {
-    p0 = finish(raw_prow<V>(pb + rowo(r0 - 1), lane));
-    p1 = finish(raw_prow<V>(pb + rowo(r0), lane));
+    p0 = finish_p<T>(raw_prow<V>(pb + rowo(r0 - 1), lane));
+    p1 = finish_p<T>(raw_prow<V>(pb + rowo(r0), lane));
     px = raw_prow<V>(pb + rowo(r0 + 1), lane);
   }
   double s = 0.0;
@@ -2519,7 +2528,7 @@ __global__ __launch_bounds__(256) void k_mg_resnorm(MgArgs<T> g) {
     T fv[V];
     vload<T, V>(fb + rowo(r) + V * lane, fv);
     const Row<T, V> w2 = finish(nx);
-    if constexpr (MULTI) p2 = finish(px);
+    if constexpr (MULTI) p2 = finish_p<T>(px);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T rr = fv[k] - kapply<T, V, MULTI>(w0, w1, w2, p0, p1, p2, k, ks, tab);
