@@ -109,30 +109,35 @@ struct TailFast {
   __device__ __forceinline__ int Hk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Ht, k); }
   __device__ __forceinline__ int Nk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Wt, k); }
 
+  // p: byte offset of a pattern's table row (pat(): pattern * kTS * sizeof(T)), so a table read is one
+  // ds_read at p with the tap as its immediate offset
+  __device__ __forceinline__ T tb(const T* t, int p, int d) const {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(t) + p + d * (int)sizeof(T));
+  }
   __device__ __forceinline__ T omega(int p) const {
-    if constexpr (MULTI) return ktb[p * kTS + 9];
+    if constexpr (MULTI) return tb(ktb, p, 9);
     return om0;
   }
   __device__ __forceinline__ T kw(int p, int d) const {
-    if constexpr (MULTI) return ktb[p * kTS + d];
+    if constexpr (MULTI) return tb(ktb, p, d);
     return kr[d];
   }
   __device__ __forceinline__ T rw(int p, int d) const {
-    if constexpr (MULTI) return rtb[p * kTS + d];
+    if constexpr (MULTI) return tb(rtb, p, d);
     return rr[d];
   }
   __device__ __forceinline__ T pw(int p, int d) const {
-    if constexpr (MULTI) return ptb[p * kTS + d];
+    if constexpr (MULTI) return tb(ptb, p, d);
     return pr[d];
   }
   __device__ __forceinline__ bool inside(int H, int N, int y) const {
     return y >= 1 && y <= H - 2 && lane >= 1 && lane <= N - 2;
   }
-  // pattern id of node (y, lane) of a level (0 off the level), loaded unconditionally
+  // table-row byte offset of node (y, lane)'s pattern (0 off the level), loaded unconditionally
   __device__ __forceinline__ int pat(const uint8_t* pk, int H, int N, int y) const {
     if constexpr (MULTI) {
       const int p = pk[min(max(y, 0), H - 1) * N + min(lane, N - 1)];
-      return (y >= 0 && y < H && lane < N) ? p : 0;
+      return (y >= 0 && y < H && lane < N) ? p * (kTS * (int)sizeof(T)) : 0;
     }
     return 0;
   }
@@ -297,8 +302,8 @@ struct TailFast {
       ea[c] = (iin && Ja >= 1 && Ja <= Nc - 2) ? va : T(0);
       eb[c] = (iin && Jb >= 1 && Jb <= Nc - 2) ? vb : T(0);
       if constexpr (MULTI) {
-        pa[c] = pkc[Ic * Nc + jA];
-        pb[c] = pkc[Ic * Nc + jB];
+        pa[c] = pkc[Ic * Nc + jA] * (kTS * (int)sizeof(T));
+        pb[c] = pkc[Ic * Nc + jB] * (kTS * (int)sizeof(T));
       } else {
         pa[c] = pb[c] = 0;
       }
