@@ -430,7 +430,9 @@ __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, co
 // FIX65: the V(1,1) 65^2 / 6-level tail of every BASELINE configuration only — a kernel of its own, so the
 // register allocation is that path's alone (sharing one kernel with the general paths spilled 16 VGPRs of
 // the fp64 single-pattern variant to scratch, reloaded inside the phases).
-template <typename T, bool MULTI, bool FIX65 = false>
+// FAST: any V(1,1) tail (the fused row-wave path) as a kernel without the general path, for the same reason
+// (sharing one kernel spilled 68 B per lane of the fp64 single-pattern variant: C2's 65 -> 33 tail took 11.2 us).
+template <typename T, bool MULTI, bool FIX65 = false, bool FAST = false>
 __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kTailLdsBytes];
   const int tid = threadIdx.x;
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
 
   // V(1,1) (the default MultiGrid.Step / iterate schedule) runs the fused row-wave path below; it
   // masks every read outside a level's interior, so only the general path needs zeroed buffers
-  const bool fast = FIX65 || (a.nu1 == 1 && a.nu2 == 1 && !a.q2);
+  const bool fast = FIX65 || FAST || (a.nu1 == 1 && a.nu2 == 1 && !a.q2);
   if (!fast) {
     for (int i = tid; i < 3 * tot; i += kTailThreads) va[i] = T(0);
     FEA_TAIL_SYNC();  // the zero fill must land before f_t is staged into the same region
@@ -665,9 +667,12 @@ static inline bool tail_dim_ok(int n, int nlev) {
                   q2};                                                                                        \
     const bool fix65 = Ht == 65 && Wt == 65 && nlev == 6 && nu1 == 1 && nu2 == 1 && !q2;                     \
     hipStream_t s_ = (hipStream_t)stream;                                                                     \
+    const bool v11 = nu1 == 1 && nu2 == 1 && !q2;                                                             \
     if (multi && fix65) k_mg_coarse_tail<T, true, true><<<B, kTailThreads, 0, s_>>>(a);                       \
+    else if (multi && v11) k_mg_coarse_tail<T, true, false, true><<<B, kTailThreads, 0, s_>>>(a);             \
     else if (multi) k_mg_coarse_tail<T, true><<<B, kTailThreads, 0, s_>>>(a);                                  \
     else if (fix65) k_mg_coarse_tail<T, false, true><<<B, kTailThreads, 0, s_>>>(a);                          \
+    else if (v11) k_mg_coarse_tail<T, false, false, true><<<B, kTailThreads, 0, s_>>>(a);                     \
     else k_mg_coarse_tail<T, false><<<B, kTailThreads, 0, s_>>>(a);                                            \
     FEA_LAUNCH_CHECK();                                                                                       \
   }
