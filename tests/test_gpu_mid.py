@@ -40,10 +40,8 @@ CASES = [  # (n, m, k, down tile, up tile); a region row must fit one wave (<= 6
 @pytest.mark.parametrize("B", [1, 3])
 def test_mid_down_bitwise(T, problem, learned, n, m, k, tile, tile_up, B):
     from feanet_amd import _lib
-    if problem == "interface" and (n != m or n > 256):
-        pytest.skip("two-material problem: square, oracle pattern search kept small")
-    if B == 3 and n > 256:
-        pytest.skip("batch covered at smaller sizes")
+    if problem == "interface" and n != m:
+        pytest.skip("two-material problem is square")
     rng = np.random.default_rng(n + 7 * k + B)
     ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned)
     nt = ktab.shape[0]
@@ -75,10 +73,8 @@ def test_mid_down_bitwise(T, problem, learned, n, m, k, tile, tile_up, B):
 @pytest.mark.parametrize("B", [1, 3])
 def test_mid_up_bitwise(T, problem, learned, n, m, k, tile_down, tile, B):
     from feanet_amd import _lib
-    if problem == "interface" and (n != m or n > 256):
-        pytest.skip("two-material problem: square, oracle pattern search kept small")
-    if B == 3 and n > 256:
-        pytest.skip("batch covered at smaller sizes")
+    if problem == "interface" and n != m:
+        pytest.skip("two-material problem is square")
     rng = np.random.default_rng(3 * n + k + B)
     npdt = np.float32 if T == torch.float32 else np.float64
     ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned)
