@@ -568,6 +568,13 @@ class MultigridSolver:
                 r -= b
         return blocks
 
+    @staticmethod
+    def pipe_blocks(njoin, G):
+        """Block sizes of vcycle(njoin): as many blocks of G as fit, then the remainder as ONE block (one graph
+        per remainder size, at most G of them): a call of k <= G cycles is a single graph launch, so its fixed
+        cost (the submission of the first graph, the gap in front of every further graph) is paid once."""
+        return [G] * (njoin // G) + ([njoin % G] if njoin % G else [])
+
     def _ensure_c(self):
         """The finest level's third buffer with the Dirichlet values of the iterate buffers a/b on its boundary
         nodes (its interior is always written before it is read; a set_boundary() not yet followed by a load()
@@ -615,8 +622,8 @@ class MultigridSolver:
         separate first pre-smooth nor a last post-smooth: every call, whatever k, runs exactly k cycles'
         work at the steady-state rate.  From a loaded iterate the first call opens the pipeline with that
         pre-smooth (fea_mg_sweep_restrict).  The end iterate is materialised only when asked for
-        (_iterate).  Replayed as few HIP graphs: blocks of GRAPH_CYCLES joins plus the binary
-        decomposition of the rest (graph_blocks), keyed by (pipeline opened?, buffer, size)."""
+        (_iterate).  Replayed as few HIP graphs: blocks of GRAPH_CYCLES joins plus one block of the rest
+        (pipe_blocks), keyed by (pipeline opened?, buffer, size)."""
         other = lambda b: "b" if b == "a" else "a"
         plan, _ = self._plan("a")
         mid = plan[1:-1]  # levels >= 1 (they never touch the finest level's iterate buffers)
@@ -629,7 +636,7 @@ class MultigridSolver:
             head, pre = [], self._mid["pre"]
         G = max(1, self.GRAPH_CYCLES)
         G = 1 << (G.bit_length() - 1)
-        for nb in self.graph_blocks(k, G):
+        for nb in self.pipe_blocks(k, G):
             key = ("pipe", bool(head), pre, nb)
             g = self._graphs.get(key)
             if g is not None:
