@@ -267,3 +267,16 @@ def test_level_pairing_equals_per_level(problem, groups, npairs):
     ref = interpret(mg, steps, v, f)[0][end]
     out = interpret(mg, paired, v, f)[0][end]
     np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 20, 31, 32, 33, 64, 100, 1000])
+def test_vcycle_blocks_cover_k(k):
+    """vcycle(k) replays blocks of GRAPH_CYCLES joined cycles plus one block of the rest (pipe_blocks), and
+    solve() the binary decomposition (graph_blocks): both cover exactly k cycles with at most G per block."""
+    from feanet_amd.solver import MultigridSolver
+    G = MultigridSolver.GRAPH_CYCLES
+    pb = MultigridSolver.pipe_blocks(k, G)
+    assert sum(pb) == k and all(0 < b <= G for b in pb)
+    assert sum(b != G for b in pb) <= 1 and (pb[-1] == k % G if k % G else pb[-1] == G)
+    gb = MultigridSolver.graph_blocks(k, G)
+    assert sum(gb) == k and all(b & (b - 1) == 0 for b in gb)
