@@ -109,12 +109,19 @@ class _FusedIterate(torch.autograd.Function):
         x, f = ctx.saved_tensors
         mg = ctx.mg
         params = (mg.conv.net.weight, mg.deconv.net.weight, mg.w)
-        with torch.enable_grad():
-            xd = x.detach().requires_grad_(ctx.needs_input_grad[0])
-            fd = f.detach().requires_grad_(ctx.needs_input_grad[1])
-            out = mg.iterate_modules(xd, fd)
-            wanted = [t for t, need in zip((xd, fd) + params, ctx.needs_input_grad[:5]) if need]
-            got = iter(torch.autograd.grad(out, wanted, g, allow_unused=True))
+        # the recompute writes the per-level fields of mg.grids; put the forward's back afterwards so the
+        # module keeps no backward-time tensors (nor the autograd graph they would hold alive)
+        saved = {j: (gr.v, gr.f) for j, gr in mg.grids.items()}
+        try:
+            with torch.enable_grad():
+                xd = x.detach().requires_grad_(ctx.needs_input_grad[0])
+                fd = f.detach().requires_grad_(ctx.needs_input_grad[1])
+                out = mg.iterate_modules(xd, fd)
+                wanted = [t for t, need in zip((xd, fd) + params, ctx.needs_input_grad[:5]) if need]
+                got = iter(torch.autograd.grad(out, wanted, g, allow_unused=True))
+        finally:
+            for j, (v, fj) in saved.items():
+                mg.grids[j].v, mg.grids[j].f = v, fj
         return tuple(next(got) if need else None for need in ctx.needs_input_grad[:5]) + (None,)
 
 
@@ -139,6 +146,7 @@ class MultiGrid(nn.Module):
         self.w.requires_grad_(False)
         self._solver = None
         self._solver_key = None
+        self._solver_ver = None
 
     def GridDict(self):
         return {i: SingleGrid(self.size, int(self.n_arr[i])) for i in range(self.L)}
@@ -180,16 +188,29 @@ class MultiGrid(nn.Module):
         return self.iterate(U, self.f)
 
     # ------------------------------------------------------------------ V-cycle
+    def _transfer_version(self):
+        return tuple((t.data_ptr(), t._version) for t in (self.conv.net.weight, self.deconv.net.weight, self.w))
+
     def _fused(self, x):
+        """The MultigridSolver of this batch shape, built once.  An optimizer step changes R / P in place
+        (their _version moves): the new values are copied into the solver's resident tables
+        (MultigridSolver.set_transfer) instead of rebuilding it, so level buffers, pattern maps and captured
+        graphs are reused across training steps; the ratios w are read back to the host only when they change."""
         from feanet_amd.solver import MultigridSolver
-        key = (x.shape[0], x.dtype, x.device, self.conv.net.weight.data_ptr(), self.deconv.net.weight.data_ptr(),
-               float(self.w[0]), float(self.w[1]), self.conv.net.weight._version, self.deconv.net.weight._version)
+        key = (x.shape[0], x.dtype, x.device)
+        ver = self._transfer_version()
         if self._solver is None or self._solver_key != key:
             self._solver = MultigridSolver(self.n, levels=self.L, problem="interface", dtype=x.dtype,
                                            device=x.device, batch=x.shape[0], size=self.size,
                                            R=self.conv.net.weight[0], P=self.deconv.net.weight[:, 0],
                                            w=(float(self.w[0]), float(self.w[1])))
             self._solver_key = key
+        elif ver != self._solver_ver:
+            old = self._solver_ver
+            self._solver.set_transfer(R=self.conv.net.weight[0] if ver[0] != old[0] else None,
+                                      P=self.deconv.net.weight[:, 0] if ver[1] != old[1] else None,
+                                      w=self.w if ver[2] != old[2] else None)
+        self._solver_ver = ver
         return self._solver
 
     def iterate(self, x, f):

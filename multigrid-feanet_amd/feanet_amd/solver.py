@@ -354,6 +354,32 @@ class MultigridSolver:
                   torch.cuda.current_stream(self.device).cuda_stream)
         return self.norm_out.clone()
 
+    def set_transfer(self, R=None, P=None, w=None):
+        """Replace the restriction / prolongation kernels (and the ratios w) of a built solver, for training
+        loops that update them between V-cycles (FEANet/multigrid.py:132-157 under an optimizer).
+
+        R / P ([npat or 1, 3, 3], any device) are rounded to float32 like the constructor's and copied into the
+        resident tables IN PLACE on the current stream: the launch plans and captured HIP graphs hold the tables'
+        addresses, so they stay valid and nothing is reallocated or recaptured.  The ratios are passed by value
+        into the launches, so new ratios (w != the current ones) drop the plans and graphs instead; the level
+        buffers are kept either way."""
+        for src, dst, name in ((R, self.rtab, "R"), (P, self.ptab, "P")):
+            if src is None:
+                continue
+            t = torch.as_tensor(src).detach().to(device=self.device, dtype=torch.float32).reshape(-1, 9)
+            if t.shape[0] not in (1, dst.shape[0]):
+                raise ValueError(f"MultigridSolver.set_transfer: {name} has {t.shape[0]} patterns, the solver "
+                                 f"{dst.shape[0]}")
+            dst.copy_(t.to(self.dtype).expand(dst.shape[0], 9))
+        if w is not None:
+            w = [float(x) for x in (w.detach().cpu().tolist() if torch.is_tensor(w) else w)]
+            if (w[0], w[1]) != self.w:
+                self._collapse()  # the pipelined state was built with the old ratios' plans
+                self.w = (w[0], w[1])
+                self._plans.clear()
+                self._graphs.clear()
+                self._eager_runs.clear()
+
     # ------------------------------------------------------------------ schedule
     def _ptr(self, lvl, name):
         if name == OMDF:  # recomputed in the kernel (u = NULL)

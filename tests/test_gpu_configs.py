@@ -6,7 +6,8 @@ against the single-GPU path, at the configuration's own size.
                                                                    which is checked against the oracle
   C5  256 x 1025^2 fp32 batch                                   -> bitwise per-sample independence,
                                                                    oracle fp32 first cycle of 3 samples,
-                                                                   their residual norms over 3 cycles
+                                                                   fp64 oracle over 3 cycles within
+                                                                   cond(K) * u32 (forward-error bound)
 """
 import os
 
@@ -154,29 +155,31 @@ def test_c5_batch256_1025_fp32():
         s1.load()
         s1.vcycle(3)
         assert torch.equal(s1.solution()[0], ub[b]), b
-    # the oracle's fp32 MultiGrid.Step on three of the samples, first cycle (as test_gpu_mg's fp32
-    # cycles: later fp32 iterates of two implementations drift apart by cond(K) eps32, and with these
-    # smooth sources the residual after 3 cycles is already at that rounding floor, so it is not compared);
-    # the batch-256 run is bitwise these samples' own runs (above)
+    # three of the samples against the oracle's MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372).
+    # Cycle 1 (from zero) against the fp32 oracle to 2e-5.  Every cycle against an fp64 oracle run of the same
+    # cycles, with the forward-error bound of a backward-stable fp32 solve of K u = f:
+    #     max|v32 - v64| <= cond(K) * u32 * max|v64|,   cond(K) = lambda_max / lambda_min = 4 / (2 pi^2 / n^2)
+    # (the Q1 stiffness stencil's eigenvalues (8 - 2 cos a - 2 cos b - 4 cos a cos b) / 3 lie in [2 pi^2/n^2, 4];
+    # u32 = 2^-24), i.e. 1.27e-2 at n = 1024.  The V-cycle contracts the error of every earlier cycle, so the
+    # bound does not grow with k.  Measured on the oracle's own fp32 path: 3e-7, 7e-4, 7e-4 after cycles 1-3;
+    # one cycle's change of the iterate is 12-17 % (cycle 2) and 1.6-3.3 % (cycle 3) of max|v|, so the bound
+    # separates a missing or repeated cycle from rounding.  The batch-256 run is bitwise these samples' own runs.
     idx = [0, 97, 255]
     s3 = MultigridSolver(n, dtype=torch.float32, batch=3)
     s3.set_rhs(f=f[idx])
     s3.load()
-    mg = orc.OracleMultigrid(n, "poisson", np.float32)
     fb = f[idx, 0].cpu().numpy()
-    r0 = orc.interior_norm(fb - mg.levels[0].K(np.zeros_like(fb)))
-    v = np.zeros_like(fb)
+    tol = 4.0 / (2.0 * np.pi ** 2 / n ** 2) * 2.0 ** -24
+    mg64 = orc.OracleMultigrid(n, "poisson", np.float64)
+    v32 = orc.OracleMultigrid(n, "poisson", np.float32).step(np.zeros_like(fb), fb)
+    v = np.zeros(fb.shape)
     for k in range(3):
         s3.vcycle()
-        v = mg.step(v, fb)
-        if k == 0:
-            got = s3.solution().cpu().numpy()[:, 0]
-            for i in range(3):
-                err = np.abs(got[i] - v[i]).max() / np.abs(v[i]).max()
+        v = mg64.step(v, fb.astype(np.float64))
+        got = s3.solution().cpu().numpy()[:, 0]
+        for i in range(3):
+            if k == 0:
+                err = np.abs(got[i] - v32[i]).max() / np.abs(v32[i]).max()
                 assert err < 2e-5, (idx[i], err)
-        # residual norms of every cycle to 1 % + 1e-3 of the initial residual: with these smooth sources r is a
-        # small difference of large K u terms, and two fp32 implementations' iterates differ by cond(K) eps32,
-        # so the two residuals differ by ~1e-5 absolute (0.5 % after one cycle, 3 % after three, where r has
-        # come down to ~1e-4, measured); a wrong schedule changes the per-cycle contraction (~0.2) far more
-        np.testing.assert_allclose(s3.residual_norm().cpu().numpy(), orc.interior_norm(fb - mg.levels[0].K(v)),
-                                   rtol=1e-2, atol=1e-3 * float(r0.max()), err_msg=f"cycle {k + 1}")
+            err = np.abs(got[i].astype(np.float64) - v[i]).max() / np.abs(v[i]).max()
+            assert err < tol, (f"cycle {k + 1}", idx[i], err, tol)
