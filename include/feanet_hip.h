@@ -325,6 +325,22 @@ int fea_mg_prolong_add_f64(const double* u, const double* ec, double* out, const
                            const double* ptab, int nptab, double w1, int B, int H, int W, int ld, long long bstride,
                            int ldc, long long bstridec, void* stream);
 
+/* The cycle join (fea_mg_cycle_join, no residual norm) over nrect <= 4 rectangles of the grid in one launch:
+ * rects[4 r ..] = {I0, I1, c0, c1}: coarse rows [I0, I1) (their fine rows 2I-1, 2I; row H-2 with I1 = Hc-1) and
+ * fine columns [c0, c1), c0 and c1 odd (coarse column J with fine columns 2J-1, 2J).  Rectangles covering the
+ * grid give fea_mg_cycle_join's result bitwise; a domain-decomposed rank computes the border strips its halo
+ * exchange sends first and the interior while the messages are in flight (feanet_amd.dd). */
+int fea_mg_cycle_join_rects_f32(const float* u, const float* ec, const float* f, float* u_out, float* fc,
+                                const uint8_t* pid, const uint8_t* pidc, const float* ktab, const float* omd, int ntab,
+                                const float* ptab, int nptab, const float* rtab, int nrtab, float w1, float w0, int B,
+                                int H, int W, int ld, long long bstride, int ldc, long long bstridec, int nrect,
+                                const int* rects, void* stream);
+int fea_mg_cycle_join_rects_f64(const double* u, const double* ec, const double* f, double* u_out, double* fc,
+                                const uint8_t* pid, const uint8_t* pidc, const double* ktab, const double* omd,
+                                int ntab, const double* ptab, int nptab, const double* rtab, int nrtab, double w1,
+                                double w0, int B, int H, int W, int ld, long long bstride, int ldc, long long bstridec,
+                                int nrect, const int* rects, void* stream);
+
 /* out[b] = || (f - K u)[b, rlo:rhi, 1:-1] ||_2 (rows rlo..rhi-1; rlo = rhi = 0: all interior rows,
  * the drivers' [1:-1, 1:-1]; likewise columns clo..chi-1, clo = chi = 0: all interior columns),
  * deterministic; ws >= fea_norm_workspace_bytes(B, H, W).  Row and column ranges give a
@@ -349,6 +365,31 @@ int fea_mg_hsweep_f32(const float* u, const float* u_raw, const float* f, float*
 int fea_mg_hsweep_f64(const double* u, const double* u_raw, const double* f, double* out, const uint8_t* pid,
                       const double* ktab, const double* omd, int ntab, const double* hw, int nlayers, int B,
                       int H, int W, int ld, long long bstride, void* stream);
+/* The learned smoother fused with the inter-grid transfers around it (the streamed MG-HJac level pair of
+ * M-FEANet-mg_test.ipynb MultiGrid.Step :27346-27372, one pass each instead of two):
+ * hsweep_restrict: out = HRelax(u) as fea_mg_hsweep (u NULL: zero guess; u_raw as there), then
+ *   fc = w0 R(f - K out) on the (H+1)/2 x (W+1)/2 level (framed ldc, bsc) as fea_mg_residual_restrict with a
+ *   stored iterate.  prolong_hsweep: x = u + w1 P(ec) on the interior (fea_mg_prolong_add, ec = the coarse
+ *   correction), then out = HRelax(x); u_raw as for fea_mg_hsweep (the first sweep of a cycle after a load with
+ *   no pre-sweep sees the un-reset guess on the boundary).  Both bitwise the two launches they replace; H, W odd; out != u. */
+int fea_mg_hsweep_restrict_f32(const float* u, const float* u_raw, const float* f, float* out, float* fc,
+                               const uint8_t* pid, const float* ktab, const float* omd, int ntab, const float* hw,
+                               int nlayers, const float* rtab, int nrtab, float w0, int B, int H, int W, int ld,
+                               long long bstride, int ldc, long long bstridec, void* stream);
+int fea_mg_hsweep_restrict_f64(const double* u, const double* u_raw, const double* f, double* out, double* fc,
+                               const uint8_t* pid, const double* ktab, const double* omd, int ntab, const double* hw,
+                               int nlayers, const double* rtab, int nrtab, double w0, int B, int H, int W, int ld,
+                               long long bstride, int ldc, long long bstridec, void* stream);
+int fea_mg_prolong_hsweep_f32(const float* u, const float* u_raw, const float* ec, const float* f, float* out,
+                              const uint8_t* pid,
+                              const uint8_t* pidc, const float* ktab, const float* omd, int ntab, const float* hw,
+                              int nlayers, const float* ptab, int nptab, float w1, int B, int H, int W, int ld,
+                              long long bstride, int ldc, long long bstridec, void* stream);
+int fea_mg_prolong_hsweep_f64(const double* u, const double* u_raw, const double* ec, const double* f, double* out,
+                              const uint8_t* pid,
+                              const uint8_t* pidc, const double* ktab, const double* omd, int ntab, const double* hw,
+                              int nlayers, const double* ptab, int nptab, double w1, int B, int H, int W, int ld,
+                              long long bstride, int ldc, long long bstridec, void* stream);
 
 /* The whole coarse end of the V-cycle (levels t..t+nlev-1 of an Ht x Wt level, Ht, Wt <= 65 and
  * (Ht-1), (Wt-1) divisible by 2^(nlev-1)) in ONE launch,
@@ -368,6 +409,24 @@ int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Ht, int Wt, int n
                            int q2, int B, void* stream);
 /* LDS bytes the coarse tail needs for (Ht, Wt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
 size_t fea_mg_coarse_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi);
+
+/* The coarse end of the learned-smoother V-cycle (MultiGrid.Step mode='hjac', M-FEANet-mg_test.ipynb:27346-27372
+ * with Relax = HJacIterator.HRelax :147-155) for levels t..t+nlev-1 of an Ht x Wt level (Ht, Wt <= 65) in ONE
+ * launch, one 1024-thread workgroup per sample, every level resident in LDS (hjac_tail.hip).  From a zero guess:
+ * nu1 HRelax pre-sweeps per level, residual + restriction, nu1+nu2 sweeps on the coarsest, prolongation +
+ * correction + nu2 post-sweeps; hw = nlayers 3x3 HNet weights.  Bitwise the per-level fea_mg_hsweep /
+ * fea_mg_residual_restrict / fea_mg_prolong_add sequence it replaces (feanet_amd.schedule.hjac_schedule).
+ * f_t / u_t: framed level-t buffers (ld_t, bs_t); u_t's interior is written.  pid_levels as for the coarse tail. */
+int fea_mg_hjac_tail_f32(const float* f_t, float* u_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
+                         const uint8_t* pid_levels, const float* ktab, const float* omd, int ntab, const float* rtab,
+                         const float* ptab, const float* hw, int nlayers, float w0, float w1, int nu1, int nu2, int B,
+                         void* stream);
+int fea_mg_hjac_tail_f64(const double* f_t, double* u_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
+                         const uint8_t* pid_levels, const double* ktab, const double* omd, int ntab,
+                         const double* rtab, const double* ptab, const double* hw, int nlayers, double w0, double w1,
+                         int nu1, int nu2, int B, void* stream);
+/* LDS bytes the learned-smoother tail needs for (Ht, Wt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
+size_t fea_mg_hjac_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi);
 
 /* Several consecutive coarse levels in ONE launch (mid_ops.hip; tiles with recomputed halos, bitwise
  * the per-level kernels).  Levels a .. a+k (k <= 4) are framed buffers (fea_mg_layout) of H x W,

@@ -266,6 +266,12 @@ struct MgArgs {
   int rlo, rhi;      // row range of the residual norm
   int clo, chi;      // column range of the residual norm
   int nt;            // 1: nontemporal stores (level larger than FEANET_NT_BYTES); 2: also loads (sweep, join)
+  // cycle join over up to 4 rectangles (nrect > 0; a domain-decomposed rank's border strips, then its interior):
+  // rectangle r = coarse rows [rI0[r], rI1[r]) x fine columns [rc0[r], rc1[r]) (odd bounds, coarse column J owned
+  // with its fine columns 2J-1, 2J), its nstrips rns[r], its row tasks rnt[r]; the launch's tasks per sample are
+  // rectangle by rectangle, rt[r] the first of rectangle r
+  int nrect;
+  int rI0[4], rI1[4], rc0[4], rc1[4], rns[4], rt[5];
 };
 
 struct TaskId {
@@ -1090,20 +1096,24 @@ struct Ovl2 {
   static constexpr int S = ((64 * V - 6 - HLC) / 4) * 4;     // owned fine columns per strip (fp64 116, fp32 244)
 };
 
-template <typename T, bool MULTI>
-__global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
+// ZR2 ALT: odd row tasks stream bottom-up, so two vertically adjacent tasks reach the fine rows both load
+// (3 + 1 rows of the intermediate level are recomputed per task) at the same moment — both at their start
+// or both at their end — and the second read of those rows is an L2 hit (k_mg_cycle_join does the same).
+#ifndef FEA_ZR2_ALT
+#define FEA_ZR2_ALT 1
+#endif
+constexpr bool kZr2Alternate = FEA_ZR2_ALT != 0;
+
+// One row task of k_mg_zero_restrict2.  REV: rows are streamed bottom-up (row step S = -1); every node value
+// is the same expression as in the forward task: stencil windows are passed in grid order, and each
+// restriction sums its three residual rows in grid order (ky = 0, 1, 2) once all three are formed.
+template <typename T, bool MULTI, bool REV>
+__device__ __forceinline__ void zr2_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* rtb) {
   using F = Frame<T>;
   using O = Ovl2<T>;
   constexpr int V = F::VEC;
   constexpr int Q = O::Q;
-  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  if constexpr (MULTI) {
-    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
-    __syncthreads();
-  }
-  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
-  if (!id.valid) return;
+  constexpr int S = REV ? -1 : 1;  // row step
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc, Hc2 = g.Hc2, Wc2 = g.Wc2;
   const int c0 = 1 + id.s * O::S;  // first owned fine column
@@ -1174,23 +1184,26 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
     if constexpr (MULTI) w.p = own_prow<T, V>(r.p);
     return w;
   };
-  auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
+  // residual of the window's middle row; x0 is the oldest row streamed (the top one unless REV)
+  auto resid = [&](const Wn& x0, const Wn& x1, const Wn& x2, T (&r)[V + 1]) {
+    const Wn& a = REV ? x2 : x0;
+    const Wn& c = REV ? x0 : x2;
 #pragma unroll
-    for (int k = 0; k < V; ++k) r[k] = b.f[k] - kapply<T, V, MULTI>(a.v, b.v, c.v, a.p, b.p, c.p, k, ks, tab);
+    for (int k = 0; k < V; ++k) r[k] = x1.f[k] - kapply<T, V, MULTI>(a.v, x1.v, c.v, a.p, x1.p, c.p, k, ks, tab);
     r[V] = shl1(r[0], T(0));
   };
 
-  // ---- stage 2 (level l+1): v' window rows I-2, I-1, I; residual rows of the current coarse-row pair
+  // ---- stage 2 (level l+1): v' window rows (streaming order, Va oldest); residual rows of f_{l+2}'s row pair
   Row<T, Q> Va{}, Vb{}, Vc{};
   PRow<Q> Qa{}, Qb{}, Qc{};
-  T fp2[Q];  // f_{l+1} of the previous row
-  Row<T, Q> Ro{}, Re{};  // the last odd and even residual rows of level l+1 (2K-1, 2K while row K forms)
+  T fp2[Q];  // f_{l+1} of the previous row pushed
+  Row<T, Q> Ro{}, Re{};  // the last odd / even residual rows of level l+1
   PRow<Q> So{}, Se{};    // their patterns
 #pragma unroll
   for (int q = 0; q < Q; ++q) fp2[q] = T(0);
 
   // push f_{l+1} row I (all lanes, exact on the valid ones); n = rows pushed before it
-  // ODD: parity of I, a compile-time constant (Ia is even), so the residual-row rotation below is static
+  // ODD: parity of I, a compile-time constant (the first row is even), so the residual-row rotation is static
   auto push = [&](int I, const T (&o)[Q], int n, auto odd_c) {
     constexpr bool ODD = decltype(odd_c)::value;
     int pq[Q];
@@ -1216,41 +1229,48 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
       Qc = own_prow<T, Q>(pq);
     }
     if (n >= 2) {
-      // residual row I-1 of level l+1 (k_mg_zero_restrict's resid on the coarse values)
+      // residual row j = I - S of level l+1 (k_mg_zero_restrict's resid on the coarse values)
       T r[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) r[q] = fp2[q] - kapply<T, Q, MULTI>(Va, Vb, Vc, Qa, Qb, Qc, q, ks, tab);
+      for (int q = 0; q < Q; ++q) {
+        if constexpr (REV) r[q] = fp2[q] - kapply<T, Q, MULTI>(Vc, Vb, Va, Qc, Qb, Qa, q, ks, tab);
+        else r[q] = fp2[q] - kapply<T, Q, MULTI>(Va, Vb, Vc, Qa, Qb, Qc, q, ks, tab);
+      }
       const Row<T, Q> R = own_row<T, Q>(r);
-      const int j = I - 1;  // residual row index (odd when I is even)
+      const int j = I - S;  // residual row index (odd when I is even)
       if constexpr (!ODD) {
-        // j = 2K+1 closes f_{l+2} row K (residual rows 2K-1 = Ro, 2K = Re, 2K+1 = R)
-        const int K = (j - 1) / 2;
+        // j = 2K + S closes f_{l+2} row K: residual rows 2K-1, 2K, 2K+1 (Ro and R in streaming order)
+        const int K = (j - S) / 2;
         if (K >= K0 && K < K1) {
           // one output column per lane: fp64 the lane's own column when it is even, fp32 its second one
           constexpr int B0 = Q == 1 ? 0 : 1;     // window index of column 2M-1
           const int Jm = J0 + (Q == 1 ? 0 : 1);  // column 2M
           const int M = Jm / 2;
+          const Row<T, Q>& r0 = REV ? R : Ro;  // row 2K-1
+          const Row<T, Q>& r2 = REV ? Ro : R;  // row 2K+1
           T acc;
           if constexpr (!MULTI) {
-            acc = rs[0] * Ro.a[B0];
-            acc += rs[1] * Ro.a[B0 + 1];
-            acc += rs[2] * Ro.a[B0 + 2];
+            acc = rs[0] * r0.a[B0];
+            acc += rs[1] * r0.a[B0 + 1];
+            acc += rs[2] * r0.a[B0 + 2];
             acc += rs[3] * Re.a[B0];
             acc += rs[4] * Re.a[B0 + 1];
             acc += rs[5] * Re.a[B0 + 2];
-            acc += rs[6] * R.a[B0];
-            acc += rs[7] * R.a[B0 + 1];
-            acc += rs[8] * R.a[B0 + 2];
+            acc += rs[6] * r2.a[B0];
+            acc += rs[7] * r2.a[B0 + 1];
+            acc += rs[8] * r2.a[B0 + 2];
           } else {
-            acc = tabv(rtb, So.a[B0], 0) * Ro.a[B0];
-            acc += tabv(rtb, So.a[B0 + 1], 1) * Ro.a[B0 + 1];
-            acc += tabv(rtb, So.a[B0 + 2], 2) * Ro.a[B0 + 2];
+            const PRow<Q>& p0 = REV ? Qb : So;
+            const PRow<Q>& p2 = REV ? So : Qb;
+            acc = tabv(rtb, p0.a[B0], 0) * r0.a[B0];
+            acc += tabv(rtb, p0.a[B0 + 1], 1) * r0.a[B0 + 1];
+            acc += tabv(rtb, p0.a[B0 + 2], 2) * r0.a[B0 + 2];
             acc += tabv(rtb, Se.a[B0], 3) * Re.a[B0];
             acc += tabv(rtb, Se.a[B0 + 1], 4) * Re.a[B0 + 1];
             acc += tabv(rtb, Se.a[B0 + 2], 5) * Re.a[B0 + 2];
-            acc += tabv(rtb, Qb.a[B0], 6) * R.a[B0];
-            acc += tabv(rtb, Qb.a[B0 + 1], 7) * R.a[B0 + 1];
-            acc += tabv(rtb, Qb.a[B0 + 2], 8) * R.a[B0 + 2];
+            acc += tabv(rtb, p2.a[B0], 6) * r2.a[B0];
+            acc += tabv(rtb, p2.a[B0 + 1], 7) * r2.a[B0 + 1];
+            acc += tabv(rtb, p2.a[B0 + 2], 8) * r2.a[B0 + 2];
           }
           if (!(Jm & 1) && M >= Mlo && M < Mhi && M <= Wc2 - 2) cb2[(long long)(K + 1) * g.ldc2 + M] = w0 * acc;
         }
@@ -1266,35 +1286,40 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
   };
 
   const int Ia = 2 * K0 - 2, Ib = 2 * K1;  // f_{l+1} rows computed (Ia .. Ib inclusive)
-  const int y0 = 2 * Ia - 1;
-  Wn X0 = mk(load(y0 - 1), y0 - 1);
-  Wn X1 = mk(load(y0), y0);
-  Wn X2 = mk(load(y0 + 1), y0 + 1);
-  T Ra[V + 1], Rb[V + 1], Rc[V + 1];
-  PRow<V> Pa = X1.p, Pb, Pc;
-  resid(X0, X1, X2, Ra);
-  // the two fine rows of a coarse row are loaded two coarse rows ahead, in ring slots indexed by the
-  // row's parity (compile-time), as in k_mg_zero_restrict
+  const int Is = REV ? Ib : Ia;            // first row streamed
+  Wn X0 = mk(load(2 * Is - 2 * S), 2 * Is - 2 * S);
+  Wn X1 = mk(load(2 * Is - S), 2 * Is - S);
+  Wn X2 = mk(load(2 * Is), 2 * Is);
+  T Rp[V + 1], Rm[V + 1], Rn[V + 1];  // residual rows 2I - S (carried), 2I, 2I + S of the current row I
+  PRow<V> Pp = X1.p, Pm, Pn;
+  resid(X0, X1, X2, Rp);
+  // the two fine rows 2I + S, 2I + 2S of a coarse row are loaded two coarse rows ahead, in ring slots indexed
+  // by the row's parity (compile-time), as in k_mg_zero_restrict
   In ring[2][2];
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
-    ring[d][0] = load(2 * Ia + 1 + 2 * d);
-    ring[d][1] = load(2 * Ia + 2 + 2 * d);
+    ring[d][0] = load(2 * Is + S + 2 * d * S);
+    ring[d][1] = load(2 * Is + 2 * S + 2 * d * S);
   }
   auto row = [&](int I, int n, auto odd_c) {
     constexpr int SL = decltype(odd_c)::value ? 1 : 0;
-    X0 = X1;  // fine row 2I
+    X0 = X1;  // window centred on fine row 2I
     X1 = X2;
-    X2 = mk(ring[SL][0], 2 * I + 1);
-    ring[SL][0] = load(2 * I + 5);
-    resid(X0, X1, X2, Rb);
-    Pb = X1.p;
-    X0 = X1;  // fine row 2I+1
+    X2 = mk(ring[SL][0], 2 * I + S);
+    ring[SL][0] = load(2 * I + 5 * S);
+    resid(X0, X1, X2, Rm);
+    Pm = X1.p;
+    X0 = X1;  // window centred on fine row 2I + S
     X1 = X2;
-    X2 = mk(ring[SL][1], 2 * I + 2);
-    ring[SL][1] = load(2 * I + 6);
-    resid(X0, X1, X2, Rc);
-    Pc = X1.p;
+    X2 = mk(ring[SL][1], 2 * I + 2 * S);
+    ring[SL][1] = load(2 * I + 6 * S);
+    resid(X0, X1, X2, Rn);
+    Pn = X1.p;
+    // rows 2I-1 (Ra), 2I (Rm), 2I+1 (Rc) in grid order
+    const T(&Ra)[V + 1] = REV ? Rn : Rp;
+    const T(&Rc)[V + 1] = REV ? Rp : Rn;
+    const PRow<V>& Pa = REV ? Pn : Pp;
+    const PRow<V>& Pc = REV ? Pp : Pn;
     T o[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -1303,9 +1328,9 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
         acc = rs[0] * Ra[2 * q];
         acc += rs[1] * Ra[2 * q + 1];
         acc += rs[2] * Ra[2 * q + 2];
-        acc += rs[3] * Rb[2 * q];
-        acc += rs[4] * Rb[2 * q + 1];
-        acc += rs[5] * Rb[2 * q + 2];
+        acc += rs[3] * Rm[2 * q];
+        acc += rs[4] * Rm[2 * q + 1];
+        acc += rs[5] * Rm[2 * q + 2];
         acc += rs[6] * Rc[2 * q];
         acc += rs[7] * Rc[2 * q + 1];
         acc += rs[8] * Rc[2 * q + 2];
@@ -1313,9 +1338,9 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
         acc = tabv(rtb, Pa.a[2 * q + 1], 0) * Ra[2 * q];
         acc += tabv(rtb, Pa.a[2 * q + 2], 1) * Ra[2 * q + 1];
         acc += tabv(rtb, Pa.a[2 * q + 3], 2) * Ra[2 * q + 2];
-        acc += tabv(rtb, Pb.a[2 * q + 1], 3) * Rb[2 * q];
-        acc += tabv(rtb, Pb.a[2 * q + 2], 4) * Rb[2 * q + 1];
-        acc += tabv(rtb, Pb.a[2 * q + 3], 5) * Rb[2 * q + 2];
+        acc += tabv(rtb, Pm.a[2 * q + 1], 3) * Rm[2 * q];
+        acc += tabv(rtb, Pm.a[2 * q + 2], 4) * Rm[2 * q + 1];
+        acc += tabv(rtb, Pm.a[2 * q + 3], 5) * Rm[2 * q + 2];
         acc += tabv(rtb, Pc.a[2 * q + 1], 6) * Rc[2 * q];
         acc += tabv(rtb, Pc.a[2 * q + 2], 7) * Rc[2 * q + 1];
         acc += tabv(rtb, Pc.a[2 * q + 3], 8) * Rc[2 * q + 2];
@@ -1331,16 +1356,30 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
     }
     push(I, o, n, odd_c);
 #pragma unroll
-    for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
-    Pa = Pc;
+    for (int k = 0; k <= V; ++k) Rp[k] = Rn[k];
+    Pp = Pn;
   };
   // Ib - Ia + 1 = 2 (K1 - K0) + 3 rows: pairs (even, odd), then the last (even) row
-  int n = 0, I = Ia;
-  for (; I + 1 <= Ib; I += 2, n += 2) {
+  int n = 0, I = Is;
+  for (; REV ? I - 1 >= Ia : I + 1 <= Ib; I += 2 * S, n += 2) {
     row(I, n, std::false_type{});
-    row(I + 1, n + 1, std::true_type{});
+    row(I + S, n + 1, std::true_type{});
   }
   row(I, n, std::false_type{});
+}
+
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) void k_mg_zero_restrict2(MgArgs<T> g) {
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T rtb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, rtb, g.rtab, g.nrtab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  if (kZr2Alternate && (id.t & 1)) zr2_task<T, MULTI, true>(g, id, tab, rtb);
+  else zr2_task<T, MULTI, false>(g, id, tab, rtb);
 }
 
 // Kernel C: fused prolongation + correction (+ post-sweep):
@@ -2166,8 +2205,14 @@ struct Ovl3 {
 // traffic per launch at 4097^2 fp64, measured; nontemporal loads still allocate there).  Every node value
 // is the same expression as in the forward task: windows are passed to the stencil in grid order and
 // a coarse row's three restriction terms are summed in the forward order (ky = 0, 1, 2).
+// the part of the grid a join task covers: sample b, coarse rows [I0, I1), fine columns from c0 (the strip's first
+// owned one) up to cmax (exclusive; the rectangle's right edge)
+struct JoinTask {
+  int b, t, I0, I1, c0, cmax;
+};
+
 template <typename T, bool MULTI, bool NT, bool NORM, bool REV, bool NTF>
-__device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* rtb,
+__device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt, const T* tab, const T* rtb,
                                           const T* ptb, double& ssq) {
   constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
   constexpr int S = REV ? -1 : 1;  // row step
@@ -2177,11 +2222,13 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   constexpr int Q = V / 2;
   const int lane = lane_id();
   const int H = g.H, W = g.W, Hc = g.Hc, Wc = g.Wc;
-  const int c0 = 1 + id.s * O::S;  // first owned fine column (odd)
+  // stores stop at the rectangle's right edge (fine columns < cmax, coarse columns J <= (cmax - 1) / 2)
+  const int Ws = min(W, jt.cmax + 1), Wcs = min(Wc, (jt.cmax + 3) / 2);
+  const int c0 = jt.c0;            // first owned fine column (odd)
   const int cs = c0 - O::HL;       // first loaded column (odd)
   const int cl = cs + V * lane;    // lane's first column (odd)
-  const int I0 = 1 + id.t * (g.rb / 2);
-  const int I1 = min(I0 + g.rb / 2, Hc - 1);
+  const int I0 = jt.I0;
+  const int I1 = jt.I1;
   T ks[9], rs[9], ps[9];
   T om = 0;
   if constexpr (!MULTI) {
@@ -2199,15 +2246,15 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
   for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
   const bool own = lane >= O::L0 && lane < O::L0 + O::OWN;
   const int J0 = (cl + 1) / 2;
-  const long long boff = (long long)id.b * g.bs + F::OFF + cs;
+  const long long boff = (long long)jt.b * g.bs + F::OFF + cs;
   const T* __restrict__ ub = g.u + boff;
   const T* __restrict__ fb = g.f + boff;
   T* __restrict__ ob = g.out2 + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + F::OFF + cs : nullptr;
   const long long cboff = F::OFF + (cs + 1) / 2;  // coarse column of lane 0's first value
-  const T* __restrict__ eb = g.ec + (long long)id.b * g.bsc + cboff;
+  const T* __restrict__ eb = g.ec + (long long)jt.b * g.bsc + cboff;
   const uint8_t* __restrict__ pcb = MULTI ? g.pidc + cboff : nullptr;
-  T* __restrict__ cb = g.out + (long long)id.b * g.bsc + F::OFF + J0;
+  T* __restrict__ cb = g.out + (long long)jt.b * g.bsc + F::OFF + J0;
   const int ld = g.ld, ldc = g.ldc;
   // lanes past the grid's last fine column W - 1 (coarse: Wc - 1) load the last needed lane's columns
   // again instead of streaming columns nothing uses: the last strip of a row can be mostly outside
@@ -2347,7 +2394,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
         const int yw = y - 2 * S;
         const bool ownr = yw >= 2 * I0 - 1 && (yw < 2 * I1 - 1 || I1 == Hc - 1) && yw <= H - 2;
         sweep3(Va, Vb, Vc, P3, P2, P1, f1, keep, yw, w, own && ownr);
-        if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, W);
+        if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, Ws);
         Wa = Wb;
         Wb = Wc_;
         Wc_ = own_row<T, V>(w);
@@ -2377,12 +2424,12 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const TaskId& id, 
           auto put = [&](int I, const T (&o)[Q]) {
             if (own) {
               T* cp = cb + (long long)(I + 1) * ldc;
-              if (J0 + Q - 1 <= Wc - 2) {
+              if (J0 + Q - 1 <= Wcs - 2) {
                 vstore<T, Q, kCoarseNT && NT>(cp, o);
               } else {
 #pragma unroll
                 for (int q = 0; q < Q; ++q)
-                  if (J0 + q <= Wc - 2) cp[q] = o[q];
+                  if (J0 + q <= Wcs - 2) cp[q] = o[q];
               }
             }
           };
@@ -2469,11 +2516,38 @@ void k_mg_cycle_join(MgArgs<T> g) {
     load_tables<T>(ptb, g.ptab, nullptr, g.nptab, nullptr, nullptr, 0);
     __syncthreads();
   }
-  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  JoinTask jt;
+  bool valid;
+  if (g.nrect == 0) {
+    const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+    valid = id.valid;
+    jt.b = id.b;
+    jt.t = id.t;
+    jt.I0 = 1 + id.t * (g.rb / 2);
+    jt.I1 = min(jt.I0 + g.rb / 2, g.Hc - 1);
+    jt.c0 = 1 + id.s * Ovl3<T>::S;
+    jt.cmax = g.W - 1;
+  } else {  // rectangles: tasks of a sample rectangle by rectangle, four per workgroup (wave-uniform, scalar)
+    const int per = g.rt[g.nrect];
+    const int wpb = (per + kWaves - 1) / kWaves;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    jt.b = bid / wpb;
+    const int w = (bid - jt.b * wpb) * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    valid = w < per;
+    int r = 0;
+    while (r + 1 < g.nrect && w >= g.rt[r + 1]) ++r;
+    const int lw = w - g.rt[r];
+    jt.t = lw / g.rns[r];
+    const int sx = lw - jt.t * g.rns[r];
+    jt.I0 = g.rI0[r] + jt.t * (g.rb / 2);
+    jt.I1 = min(jt.I0 + g.rb / 2, g.rI1[r]);
+    jt.c0 = g.rc0[r] + sx * Ovl3<T>::S;
+    jt.cmax = g.rc1[r];
+  }
   double ssq = 0.0;
-  if (id.valid) {
-    if (kJoinAlternate && (id.t & 1)) join_task<T, MULTI, NT, NORM, true, NTF>(g, id, tab, rtb, ptb, ssq);
-    else join_task<T, MULTI, NT, NORM, false, NTF>(g, id, tab, rtb, ptb, ssq);
+  if (valid) {
+    if (kJoinAlternate && (jt.t & 1)) join_task<T, MULTI, NT, NORM, true, NTF>(g, jt, tab, rtb, ptb, ssq);
+    else join_task<T, MULTI, NT, NORM, false, NTF>(g, jt, tab, rtb, ptb, ssq);
   }
   if constexpr (NORM) norm_partial<T>(g, ssq);
 }
@@ -3015,6 +3089,67 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
 #define COMMA ,
 FEA_MG_API(f32, float)
 FEA_MG_API(f64, double)
+
+// The cycle join over up to four rectangles of the grid in ONE launch (a domain-decomposed rank's border strips,
+// whose nodes its halo exchange sends, ahead of the interior that runs while the messages are in flight).
+// rects: nrect x {I0, I1, c0, c1}: coarse rows [I0, I1) with their fine rows 2I-1, 2I (and row H-2 when I1 = Hc-1),
+// fine columns [c0, c1) with odd c0, c1 (coarse column J goes with fine columns 2J-1, 2J).  Every node is the same
+// expression as in the whole-grid launch, so a cover of the grid by rectangles is bitwise fea_mg_cycle_join.
+template <typename T>
+static int cycle_join_rects(const T* u, const T* ec, const T* f, T* u_out, T* fc, const uint8_t* pid,
+                            const uint8_t* pidc, const T* ktab, const T* omd, int ntab, const T* ptab, int nptab,
+                            const T* rtab, int nrtab, T w1, T w0, int B, int H, int W, int ld, long long bs, int ldc,
+                            long long bsc, int nrect, const int* rects, void* stream) {
+  if (!u || !ec || !f || !u_out || !fc || !ktab || !omd || !ptab || !rtab || B <= 0 || u_out == u || !rects ||
+      nrect < 1 || nrect > 4)
+    return FEA_EINVAL;
+  if (!layout_ok<T>(H, W, ld, bs) || !coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;
+  if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nrtab != ntab && nrtab != 1) || (nptab != ntab && nptab != 1))
+    return FEA_EINVAL;
+  const bool multi = ntab > 1;
+  if (multi && (!pid || !pidc || nrtab == 1 || nptab == 1)) return FEA_EINVAL;
+  MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);
+  g.u = u; g.ec = ec; g.f = f; g.out = fc; g.out2 = u_out; g.pid = pid; g.pidc = pidc; g.ktab = ktab;
+  g.omd = omd; g.ntab = ntab; g.ptab = ptab; g.nptab = nptab; g.rtab = rtab; g.nrtab = nrtab; g.w = w0;
+  g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;
+  if (g.nt && bs * (long long)sizeof(T) > nt_load_bytes()) g.nt = 2;
+  g.nrect = nrect;
+  for (int r = 0; r < nrect; ++r) {
+    const int I0 = rects[4 * r], I1 = rects[4 * r + 1], c0 = rects[4 * r + 2], c1 = rects[4 * r + 3];
+    if (I0 < 1 || I1 > g.Hc - 1 || I0 >= I1 || c0 < 1 || c1 > W - 1 || c0 >= c1 || !(c0 & 1) || !(c1 & 1))
+      return FEA_EINVAL;
+    g.rI0[r] = I0; g.rI1[r] = I1; g.rc0[r] = c0; g.rc1[r] = c1;
+    g.rns[r] = div_up(c1 - c0, Ovl3<T>::S);
+  }
+  // rows per task: the tallest (<= the join's cap) that still gives the launch target_waves() waves
+  auto tasks = [&](int rb) {
+    long long n = 0;
+    for (int r = 0; r < nrect; ++r) n += (long long)div_up(g.rI1[r] - g.rI0[r], rb / 2) * g.rns[r];
+    return n;
+  };
+  g.rb = join_max_rb();
+  while (g.rb > 2 && (long long)B * tasks(g.rb) < target_waves()) g.rb /= 2;
+  g.rt[0] = 0;
+  for (int r = 0; r < nrect; ++r) g.rt[r + 1] = g.rt[r] + div_up(g.rI1[r] - g.rI0[r], g.rb / 2) * g.rns[r];
+  const dim3 grid((unsigned)(B * div_up(g.rt[nrect], kWaves)));
+  hipStream_t s = (hipStream_t)stream;
+  if (multi) FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA true COMMA false)
+  else FEA_NT3_LAUNCH(k_mg_cycle_join, T COMMA false COMMA false)
+  FEA_LAUNCH_CHECK();
+}
+
+#define FEA_JOIN_RECTS_API(SUF, T)                                                                            \
+  extern "C" int fea_mg_cycle_join_rects_##SUF(const T* u, const T* ec, const T* f, T* u_out, T* fc,            \
+                                               const uint8_t* pid, const uint8_t* pidc, const T* ktab,          \
+                                               const T* omd, int ntab, const T* ptab, int nptab, const T* rtab,  \
+                                               int nrtab, T w1, T w0, int B, int H, int W, int ld, long long bs,  \
+                                               int ldc, long long bsc, int nrect, const int* rects,             \
+                                               void* stream) {                                                  \
+    return cycle_join_rects<T>(u, ec, f, u_out, fc, pid, pidc, ktab, omd, ntab, ptab, nptab, rtab, nrtab, w1, w0, \
+                               B, H, W, ld, bs, ldc, bsc, nrect, rects, stream);                               \
+  }
+FEA_JOIN_RECTS_API(f32, float)
+FEA_JOIN_RECTS_API(f64, double)
 
 // Rows per task of k_mg_zero_restrict2 (fine rows, a multiple of 4): the tallest power of two that still
 // gives kZr2Waves waves, at least kZr2MinRb (each task recomputes 3 + 1 rows of the intermediate level).

@@ -14,6 +14,8 @@
 // the same expression at every node (fp-contract=on), so results do not depend on the geometry.
 #include "fea_common.h"
 
+#include <type_traits>
+
 namespace fea {
 
 constexpr int kHMaxLayers = 3;    // HNet(nb_layers=3) (M-FEANet-mg_test.ipynb:222)
@@ -112,20 +114,46 @@ struct HSArgs {
   int H, W, ld;
   long long bs;
   int nstrips, ntr, rb;
+  // MODE 1 (prolongation + correction first): the sweep's iterate is x = u + w1 P(ec)
+  const T* ec;
+  const uint8_t* pidc;
+  const T* ptab;
+  T w1;
+  // MODE 2 (residual + restriction after): fc = w0 R(f - K out)
+  T* fc;
+  const T* rtab;
+  T w0;
+  int Hc, Wc, ldc;
+  long long bsc;
 };
 
-template <typename T, bool MULTI, bool ZERO, bool RAW, int NL>
+// MODE 0: the sweep alone (fea_mg_hsweep).
+// MODE 1: prolongation + correction + sweep (fea_mg_prolong_hsweep): the loaded row u(y) becomes
+//   x(y) = u(y) + w1 P(ec) on the interior (k_mg_prolong<SWEEP = false>'s expressions: correct_even / correct_odd)
+//   as it enters the window, so the corrected iterate is never stored.
+// MODE 2: sweep + residual + restriction (fea_mg_hsweep_restrict): out rows enter a 3-row window (boundary nodes
+//   hold the iterate's values there, as in the buffer the separate kernels would read), the residual f - K out of
+//   the middle row is formed one row later and three residual rows close a coarse row (k_mg_resid_restrict's
+//   expressions); the wave loads two more halo columns per side and a task owns rb/2 coarse rows.
+template <typename T, bool MULTI, bool ZERO, bool RAW, int NL, int MODE>
 __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
+  static_assert(MODE != 1 || !ZERO, "the prolongation variant corrects a stored iterate");
   constexpr int V = HVec<T>::V;
+  constexpr int Q = V / 2;
   constexpr int HALO = NL + 1;                 // columns / rows the stage chain reaches on each side
-  constexpr int HLN = (HALO + V - 1) / V;      // halo lanes per side
+  // MODE 1: the corrected iterate is wrong on the leftmost loaded column too (its left coarse node comes from a
+  // lane the wave does not have); MODE 2: the residual and the restriction reach one column each further
+  constexpr int HALOC = HALO + (MODE == 2 ? 2 : MODE == 1 ? 1 : 0);
+  constexpr int HLN = (HALOC + V - 1) / V;     // halo lanes per side
   constexpr int S = (64 - 2 * HLN) * V;        // owned columns per strip
   constexpr int OFF = 128 / (int)sizeof(T) - 1;
   __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kHTS : 1];
+  __shared__ T tb2[(MULTI && MODE != 0) ? FEA_MAX_PATTERNS * kHTS : 1];  // P (MODE 1) or R (MODE 2) kernels
   if constexpr (MULTI) {
     for (int i = threadIdx.x; i < g.ntab * kHTS; i += 256) {
       const int p = i / kHTS, d = i - p * kHTS;
       tab[i] = d == 9 ? g.omd[p] : g.ktab[p * 9 + d];
+      if constexpr (MODE != 0) tb2[i] = d == 9 ? T(0) : (MODE == 1 ? g.ptab : g.rtab)[p * 9 + d];
     }
     __syncthreads();
   }
@@ -143,17 +171,34 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
   const int cl = cs + V * lane;
   const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the last column re-read a valid line
   const bool own = lane >= HLN && lane < 64 - HLN;
-  const int r0 = 1 + t * g.rb, r1 = min(r0 + g.rb, H - 1);
+  // out rows owned [r0, r1) and computed [rc0, rc1)
+  int r0, r1, rc0, rc1, I0 = 0, I1 = 0;
+  if constexpr (MODE == 2) {
+    I0 = 1 + t * (g.rb / 2);
+    I1 = min(I0 + g.rb / 2, g.Hc - 1);
+    r0 = 2 * I0 - 1;
+    r1 = I1 == g.Hc - 1 ? H - 1 : 2 * I1 - 1;
+    rc0 = 2 * I0 - 2;
+    rc1 = 2 * I1 + 1;
+  } else {
+    r0 = 1 + t * g.rb;
+    r1 = min(r0 + g.rb, H - 1);
+    rc0 = r0;
+    rc1 = r1;
+  }
   bool cin[V], cgr[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     cin[k] = cl + k >= 1 && cl + k <= W - 2;
     cgr[k] = cl + k >= 0 && cl + k <= W - 1;
   }
-  T ks[9], om = 0, hk[NL > 0 ? NL : 1][9];
+  T ks[9], om = 0, hk[NL > 0 ? NL : 1][9], t2[9];
   if constexpr (!MULTI) {
 #pragma unroll
-    for (int d = 0; d < 9; ++d) ks[d] = g.ktab[d];
+    for (int d = 0; d < 9; ++d) {
+      ks[d] = g.ktab[d];
+      if constexpr (MODE != 0) t2[d] = (MODE == 1 ? g.ptab : g.rtab)[d];
+    }
     om = g.omd[0];
   }
 #pragma unroll
@@ -168,6 +213,62 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
   const uint8_t* __restrict__ pb = MULTI ? g.pid + OFF + cs : nullptr;
   auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
 
+  // MODE 1: the lane's coarse values (cl + 1) / 2 + q, q < Q, and the left lane's last one (DPP)
+  const int jc = (cs + 1) / 2;
+  const int llc = MODE == 1 ? min(lane, (g.Wc - 1 - jc) / Q) : 0;
+  const T* __restrict__ eb = MODE == 1 ? g.ec + (long long)b * g.bsc + OFF + jc + Q * llc : nullptr;
+  const uint8_t* __restrict__ pcb = (MODE == 1 && MULTI) ? g.pidc + OFF + jc + Q * llc : nullptr;
+  struct CR {  // coarse row: e[0] = column (cl-1)/2 (left lane), e[1..Q] = own; pattern offsets o[]
+    T e[Q + 1];
+    int o[Q + 1];
+  };
+  struct CRaw {
+    T x[Q];
+    int p[Q];
+  };
+  auto crow_ld = [&](int a) {
+    CRaw r;
+    const long long o = (long long)(min(max(a, -1), g.Hc) + 1) * g.ldc;
+    if constexpr (MODE == 1) {
+      if constexpr (Q == 1) {
+        r.x[0] = eb[o];
+      } else {
+        typedef T v2 __attribute__((ext_vector_type(2)));  // Q == 2: fp32, 8-byte aligned (jc is odd, OFF odd)
+        const v2 v = *reinterpret_cast<const v2*>(eb + o);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) r.x[q] = v[q];
+      }
+      if constexpr (MULTI) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) r.p[q] = pcb[o + q];
+      }
+    }
+    return r;
+  };
+  auto crow_fin = [&](const CRaw& r) {
+    CR c{};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) c.e[q + 1] = r.x[q];
+    c.e[0] = shr1(r.x[Q - 1], T(0));
+    if constexpr (MULTI) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * kHTS;
+      c.o[0] = shr1(r.p[Q - 1], 0) * kHTS;
+    }
+    return c;
+  };
+  // crow_term (framed_ops.hip) at own column k: coarse row c's contribution with row tap ky
+  auto cterm = [&](const CR& c, int k, int ky) -> T {
+    if (k & 1) {  // even fine column (cl odd): one coarse node, kx = 1
+      const int i = (k + 1) / 2;
+      return (MULTI ? tb2[c.o[i] + ky * 3 + 1] : t2[ky * 3 + 1]) * c.e[i];
+    }
+    const int i = k / 2;  // odd fine column: coarse nodes i (kx = 2) and i + 1 (kx = 0)
+    T tt = (MULTI ? tb2[c.o[i] + ky * 3 + 2] : t2[ky * 3 + 2]) * c.e[i];
+    tt += (MULTI ? tb2[c.o[i + 1] + ky * 3 + 0] : t2[ky * 3 + 0]) * c.e[i + 1];
+    return tt;
+  };
+
   HWin<T, V> U0{}, U1{}, U2{};           // u rows y-2, y-1, y
   HWin<int, V> P0{}, P1{}, P2{};         // pattern offsets of the same rows
   HWin<T, V> D[NL > 0 ? NL : 1][3] = {}; // d_l windows: d_l of rows (y-1-l)-2 .. (y-1-l)
@@ -176,25 +277,84 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
   for (int i = 0; i <= NL; ++i)
 #pragma unroll
     for (int k = 0; k < V; ++k) J[i][k] = T(0);
-  const int y0 = r0 - HALO, y1 = r1 - 1 + HALO;
-  T un[V], fn[V];
-  int pn[V];
+  // MODE 2: out windows (rows yo-2 .. yo), their patterns, the residual rows 2I-1 (Ra), 2I (Rb) of a coarse row
+  HWin<T, V> O0{}, O1{}, O2{};
+  HWin<int, V> Q0{}, Q1{}, Q2{};
+  T Ra[V + 1], Rb[V + 1];
+  HWin<int, V> PRa{}, PRb{};
 #pragma unroll
-  for (int k = 0; k < V; ++k) { un[k] = T(0); pn[k] = 0; }
-  if constexpr (!ZERO) hload<T, V>(ub + rowo(y0), un);
-  if constexpr (MULTI) hpload<V>(pb + rowo(y0), pn);
-  hload<T, V>(fb + rowo(y0 - 1), fn);
-  for (int y = y0; y <= y1; ++y) {
-    // rotate the u window in row y (loaded one step ahead); f of row y-1
-    T uy[V], fy1[V];
-    int py[V];
+  for (int k = 0; k <= V; ++k) Ra[k] = Rb[k] = T(0);
+  const int y0 = rc0 - HALO, y1 = rc1 - 1 + HALO;
+  // input rows two steps ahead, in a ring of two slots indexed by the step's parity (compile-time after the
+  // unroll below): step y consumes u(y), pid(y), f(y-1) (RAW: u_raw(y-1); MODE 2: f and pid of its residual row
+  // y-2-NL, the iterate of its out row y-1-NL) and refills the slot with the rows of step y+2 at once
+  T ur[2][V], fr_[2][V], rw_[2][V], frr[2][V], uo[2][V];
+  int pr[2][V], po[2][V];
+  // MODE 2 needs the iterate's values of an out row only where they stand in for the sweep (boundary nodes)
+  auto need_uo = [&](int yy) { return !(yy >= 1 && yy <= H - 2) || !cin[0] || !cin[V - 1]; };
+  auto fill = [&](int sl, int y) {
 #pragma unroll
-    for (int k = 0; k < V; ++k) { uy[k] = un[k]; fy1[k] = fn[k]; py[k] = pn[k]; }
-    if (y + 1 <= y1) {
-      if constexpr (!ZERO) hload<T, V>(ub + rowo(y + 1), un);
-      if constexpr (MULTI) hpload<V>(pb + rowo(y + 1), pn);
+    for (int k = 0; k < V; ++k) ur[sl][k] = T(0);
+    if constexpr (!ZERO) hload<T, V>(ub + rowo(y), ur[sl]);
+    if constexpr (MULTI) hpload<V>(pb + rowo(y), pr[sl]);
+    hload<T, V>(fb + rowo(y - 1), fr_[sl]);
+    if constexpr (RAW) hload<T, V>(rb_ + rowo(y - 1), rw_[sl]);
+    if constexpr (MODE == 2) {
+      hload<T, V>(fb + rowo(y - 2 - NL), frr[sl]);
+      if constexpr (MULTI) hpload<V>(pb + rowo(y - 1 - NL), po[sl]);
+      if constexpr (!ZERO) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) uo[sl][k] = T(0);
+        if (need_uo(y - 1 - NL)) hload<T, V>(ub + rowo(y - 1 - NL), uo[sl]);
+      }
     }
-    hload<T, V>(fb + rowo(y), fn);
+  };
+  fill(0, y0);
+  fill(1, y0 + 1);
+  // MODE 1: coarse rows floor(y/2) (Clo) and floor(y/2) + 1 (Chi) of the row entering the window; nC = the next
+  CR Clo{}, Chi{};
+  CRaw nC{};
+  if constexpr (MODE == 1) {
+    const int a0 = y0 >> 1;  // floor (y0 may be negative: rows outside the grid get no correction)
+    Clo = crow_fin(crow_ld(a0));
+    Chi = crow_fin(crow_ld(a0 + 1));
+    nC = crow_ld(a0 + 2);
+  }
+  auto step = [&](int y, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+    // this step's rows (their loads were issued two steps ago), then the slot's refill for step y+2
+    T uy[V], fy1[V], raw[V], fres[V], uout[V];
+    int py[V], pout[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      uy[k] = ur[SL][k];
+      fy1[k] = fr_[SL][k];
+      py[k] = MULTI ? pr[SL][k] : 0;
+      raw[k] = RAW ? rw_[SL][k] : T(0);
+      fres[k] = MODE == 2 ? frr[SL][k] : T(0);
+      uout[k] = (MODE == 2 && !ZERO) ? uo[SL][k] : T(0);
+      pout[k] = (MODE == 2 && MULTI) ? po[SL][k] : 0;
+    }
+    if (y + 2 <= y1) fill(SL, y + 2);
+    if constexpr (MODE == 1) {
+      // x(y) = u(y) + w1 P(ec) on the interior (correct_even / correct_odd of k_mg_prolong)
+      const bool yin = y >= 1 && y <= H - 2;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        if (!(yin && cin[k])) continue;
+        if (!(y & 1)) {
+          uy[k] += g.w1 * cterm(Clo, k, 1);
+        } else {
+          const T tt = cterm(Clo, k, 2) + cterm(Chi, k, 0);
+          uy[k] += g.w1 * tt;
+        }
+      }
+      if (y & 1) {  // the next row (even) starts the next coarse row pair
+        Clo = Chi;
+        Chi = crow_fin(nC);
+        nC = crow_ld((y >> 1) + 3);
+      }
+    }
     U0 = U1;
     U1 = U2;
     U2 = hwin<T, V>(uy);
@@ -207,10 +367,6 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
     const int yj = y - 1;
     const bool rin = yj >= 1 && yj <= H - 2, rgr = yj >= 0 && yj <= H - 1;
     T d0[V], jv[V];
-    T raw[V];
-    if constexpr (RAW) {
-      hload<T, V>(rb_ + rowo(yj), raw);
-    }
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       T acc;
@@ -257,6 +413,13 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
       D[0][1] = D[0][2];
       D[0][2] = hwin<T, V>(d0);
     }
+    // out row yo = y-1-NL: j + d_NL on the interior
+    const int yo = y - 1 - NL;
+    T o[V];
+    if constexpr (NL == 0) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = J[0][k];
+    }
     // d_l of row y-1-l from the d_(l-1) window of rows y-1-l-1 .. y-1-l+1
 #pragma unroll
     for (int l = 1; l <= NL; ++l) {
@@ -284,69 +447,174 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
         D[l][1] = D[l][2];
         D[l][2] = hwin<T, V>(dl);
       } else {
-        // out of row y-1-NL = j + d_NL on the owned interior nodes
-        const int yo = y - 1 - NL;
-        if (own && yo >= r0 && yo < r1) {
-          T o[V];
 #pragma unroll
-          for (int k = 0; k < V; ++k) o[k] = J[NL][k] + dl[k];
-          hstore<T, V>(ob + (long long)(yo + 1) * ld + V * lane, o, cin);
+        for (int k = 0; k < V; ++k) o[k] = J[NL][k] + dl[k];
+      }
+    }
+    if (own && yo >= r0 && yo < r1) hstore<T, V>(ob + (long long)(yo + 1) * ld + V * lane, o, cin);
+    if constexpr (MODE == 2) {
+      // the out row as the buffer would hold it: the iterate's own values off the interior
+      const bool oin = yo >= 1 && yo <= H - 2;
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = (oin && cin[k]) ? o[k] : uout[k];
+      O0 = O1;
+      O1 = O2;
+      O2 = hwin<T, V>(o);
+      if constexpr (MULTI) {
+        Q0 = Q1;
+        Q1 = Q2;
+        Q2 = hpwin<V>(pout);
+      }
+      // residual row yr = yo - 1 (fea_mg_residual_restrict's resid), then the restriction of its coarse row
+      const int yr = yo - 1;
+      if (yr >= rc0 + 1) {
+        T r[V + 1];
+        const T(&fr)[V] = fres;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          T acc;
+          if constexpr (!MULTI) {
+            acc = ks[0] * O0.a[k];
+            acc += ks[1] * O0.a[k + 1];
+            acc += ks[2] * O0.a[k + 2];
+            acc += ks[3] * O1.a[k];
+            acc += ks[4] * O1.a[k + 1];
+            acc += ks[5] * O1.a[k + 2];
+            acc += ks[6] * O2.a[k];
+            acc += ks[7] * O2.a[k + 1];
+            acc += ks[8] * O2.a[k + 2];
+          } else {
+            acc = tab[Q0.a[k] + 0] * O0.a[k];
+            acc += tab[Q0.a[k + 1] + 1] * O0.a[k + 1];
+            acc += tab[Q0.a[k + 2] + 2] * O0.a[k + 2];
+            acc += tab[Q1.a[k] + 3] * O1.a[k];
+            acc += tab[Q1.a[k + 1] + 4] * O1.a[k + 1];
+            acc += tab[Q1.a[k + 2] + 5] * O1.a[k + 2];
+            acc += tab[Q2.a[k] + 6] * O2.a[k];
+            acc += tab[Q2.a[k + 1] + 7] * O2.a[k + 1];
+            acc += tab[Q2.a[k + 2] + 8] * O2.a[k + 2];
+          }
+          r[k] = fr[k] - acc;
+        }
+        r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+        if ((yr & 1) == 0) {  // row 2I
+#pragma unroll
+          for (int k = 0; k <= V; ++k) Rb[k] = r[k];
+          PRb = Q1;
+        } else {
+          if (yr > rc0 + 1) {  // row 2I+1 closes coarse row I = (yr - 1) / 2
+            const int I = (yr - 1) / 2;
+            T oc[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              T acc;
+              if constexpr (!MULTI) {
+                acc = t2[0] * Ra[2 * q];
+                acc += t2[1] * Ra[2 * q + 1];
+                acc += t2[2] * Ra[2 * q + 2];
+                acc += t2[3] * Rb[2 * q];
+                acc += t2[4] * Rb[2 * q + 1];
+                acc += t2[5] * Rb[2 * q + 2];
+                acc += t2[6] * r[2 * q];
+                acc += t2[7] * r[2 * q + 1];
+                acc += t2[8] * r[2 * q + 2];
+              } else {
+                acc = tb2[PRa.a[2 * q + 1] + 0] * Ra[2 * q];
+                acc += tb2[PRa.a[2 * q + 2] + 1] * Ra[2 * q + 1];
+                acc += tb2[PRa.a[2 * q + 3] + 2] * Ra[2 * q + 2];
+                acc += tb2[PRb.a[2 * q + 1] + 3] * Rb[2 * q];
+                acc += tb2[PRb.a[2 * q + 2] + 4] * Rb[2 * q + 1];
+                acc += tb2[PRb.a[2 * q + 3] + 5] * Rb[2 * q + 2];
+                acc += tb2[Q1.a[2 * q + 1] + 6] * r[2 * q];
+                acc += tb2[Q1.a[2 * q + 2] + 7] * r[2 * q + 1];
+                acc += tb2[Q1.a[2 * q + 3] + 8] * r[2 * q + 2];
+              }
+              oc[q] = g.w0 * acc;
+            }
+            const int Jl = (cl + 1) / 2;
+            if (own && I >= I0 && I < I1) {
+              T* cp = g.fc + (long long)b * g.bsc + OFF + (long long)(I + 1) * g.ldc + Jl;
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                if (Jl + q <= g.Wc - 2) cp[q] = oc[q];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k <= V; ++k) Ra[k] = r[k];
+          PRa = Q1;
         }
       }
     }
-    if constexpr (NL == 0) {
-      const int yo = y - 1;
-      if (own && yo >= r0 && yo < r1) hstore<T, V>(ob + (long long)(yo + 1) * ld + V * lane, J[0], cin);
-    }
+  };
+  int y = y0;
+  for (; y + 1 <= y1; y += 2) {
+    step(y, std::integral_constant<int, 0>{});
+    step(y + 1, std::integral_constant<int, 1>{});
   }
+  if (y <= y1) step(y, std::integral_constant<int, 0>{});
 }
 
 }  // namespace fea
 
 using namespace fea;
 
-template <typename T, bool MULTI, bool ZERO, bool RAW>
+template <typename T, bool MULTI, bool ZERO, bool RAW, int MODE>
 static void hs_launch_nl(int nl, dim3 grid, hipStream_t s, const HSArgs<T>& g) {
   switch (nl) {
-    case 0: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 0><<<grid, 256, 0, s>>>(g); break;
-    case 1: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 1><<<grid, 256, 0, s>>>(g); break;
-    case 2: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 2><<<grid, 256, 0, s>>>(g); break;
-    default: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 3><<<grid, 256, 0, s>>>(g); break;
+    case 0: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 0, MODE><<<grid, 256, 0, s>>>(g); break;
+    case 1: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 1, MODE><<<grid, 256, 0, s>>>(g); break;
+    case 2: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 2, MODE><<<grid, 256, 0, s>>>(g); break;
+    default: k_mg_hsweep_strip<T, MULTI, ZERO, RAW, 3, MODE><<<grid, 256, 0, s>>>(g); break;
   }
 }
 
-template <typename T>
-static int hsweep_strip_launch(const T* u, const T* u_raw, const T* f, T* out, const uint8_t* pid, const T* ktab,
-                               const T* omd, int ntab, const T* hw, int nl, int B, int H, int W, int ld, long long bs,
-                               hipStream_t s) {
+template <typename T, int MODE>
+static void hs_dispatch(bool multi, bool zero, bool raw, int nl, dim3 grid, hipStream_t s, const HSArgs<T>& g) {
+  if constexpr (MODE == 1) {
+    if (raw) {
+      if (multi) hs_launch_nl<T, true, false, true, 1>(nl, grid, s, g);
+      else hs_launch_nl<T, false, false, true, 1>(nl, grid, s, g);
+    } else {
+      if (multi) hs_launch_nl<T, true, false, false, 1>(nl, grid, s, g);
+      else hs_launch_nl<T, false, false, false, 1>(nl, grid, s, g);
+    }
+  } else if (zero) {
+    if (multi) hs_launch_nl<T, true, true, false, MODE>(nl, grid, s, g);
+    else hs_launch_nl<T, false, true, false, MODE>(nl, grid, s, g);
+  } else if (raw) {
+    if (multi) hs_launch_nl<T, true, false, true, MODE>(nl, grid, s, g);
+    else hs_launch_nl<T, false, false, true, MODE>(nl, grid, s, g);
+  } else {
+    if (multi) hs_launch_nl<T, true, false, false, MODE>(nl, grid, s, g);
+    else hs_launch_nl<T, false, false, false, MODE>(nl, grid, s, g);
+  }
+}
+
+// rows per task: the largest of 64 / 32 / 16 / 8 that still gives >= 2048 waves (each task recomputes nl + 1
+// (MODE 2: nl + 2) rows above and below its own)
+template <typename T, int MODE>
+static int hsweep_launch(HSArgs<T> g, int nl, int B, hipStream_t s) {
   constexpr int V = HVec<T>::V;
-  const int hln = (nl + 1 + V - 1) / V;
+  const int hln = (nl + 1 + (MODE == 2 ? 2 : MODE == 1 ? 1 : 0) + V - 1) / V;
   const int S = (64 - 2 * hln) * V;
   // (lanes past the grid's last column re-read the last valid line: loads stay within columns < W + V)
-  HSArgs<T> g{u, u_raw, f, out, pid, ktab, omd, hw, ntab, H, W, ld, bs, 0, 0, 0};
-  g.nstrips = (W - 2 + S - 1) / S;
-  // rows per task: the largest of 64 / 32 / 16 / 8 that still gives >= 2048 waves (each task recomputes nl + 1
-  // rows above and below its own)
+  g.nstrips = (g.W - 2 + S - 1) / S;
+  const int rows = MODE == 2 ? g.Hc - 2 : g.H - 2;  // MODE 2 tasks count coarse rows (rb / 2 each)
+  const int per = MODE == 2 ? 2 : 1;
   g.rb = 8;
   for (int rb = 64; rb > 8; rb /= 2)
-    if ((long long)B * g.nstrips * ((H - 2 + rb - 1) / rb) >= 2048) {
+    if ((long long)B * g.nstrips * ((rows * per + rb - 1) / rb) >= 2048) {
       g.rb = rb;
       break;
     }
-  g.ntr = (H - 2 + g.rb - 1) / g.rb;
+  g.ntr = MODE == 2 ? (rows + g.rb / 2 - 1) / (g.rb / 2) : (rows + g.rb - 1) / g.rb;
   const dim3 grid((unsigned)(B * ((g.ntr * g.nstrips + 3) / 4)));
-  const bool multi = ntab > 1;
-  if (!u) {
-    if (multi) hs_launch_nl<T, true, true, false>(nl, grid, s, g);
-    else hs_launch_nl<T, false, true, false>(nl, grid, s, g);
-  } else if (u_raw) {
-    if (multi) hs_launch_nl<T, true, false, true>(nl, grid, s, g);
-    else hs_launch_nl<T, false, false, true>(nl, grid, s, g);
-  } else {
-    if (multi) hs_launch_nl<T, true, false, false>(nl, grid, s, g);
-    else hs_launch_nl<T, false, false, false>(nl, grid, s, g);
-  }
+  hs_dispatch<T, MODE>(g.ntab > 1, !g.u, g.u_raw != nullptr, nl, grid, s, g);
   FEA_LAUNCH_CHECK();
+}
+
+static inline bool hs_layout_ok(int H, int W, int ld, long long bs, int esz) {
+  return H >= 3 && W >= 3 && ld >= W + 128 / esz && bs >= (long long)(H + 2) * ld;
 }
 
 #define FEA_HNET_API(SUF, T)                                                                                \
@@ -355,12 +623,57 @@ static int hsweep_strip_launch(const T* u, const T* u_raw, const T* f, T* out, c
                                      const T* omd, int ntab, const T* hw, int nlayers, int B, int H, int W,  \
                                      int ld, long long bs, void* stream) {                                   \
     if (!f || !out || !ktab || !omd || (!hw && nlayers > 0) || out == u || B <= 0 || B > 65535) return FEA_EINVAL; \
-    if (H < 3 || W < 3 || nlayers < 0 || nlayers > kHMaxLayers) return FEA_EINVAL;                           \
+    if (nlayers < 0 || nlayers > kHMaxLayers || !hs_layout_ok(H, W, ld, bs, sizeof(T))) return FEA_EINVAL;    \
     if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
-    if (ld < W + 128 / (int)sizeof(T) || bs < (long long)(H + 2) * ld) return FEA_EINVAL;                     \
     if (u_raw && !u) return FEA_EINVAL;                                                                      \
-    return hsweep_strip_launch<T>(u, u_raw, f, out, pid, ktab, omd, ntab, hw, nlayers, B, H, W, ld, bs,         \
-                                  (hipStream_t)stream);                                                        \
+    HSArgs<T> g{};                                                                                           \
+    g.u = u; g.u_raw = u_raw; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.hw = hw;       \
+    g.ntab = ntab; g.H = H; g.W = W; g.ld = ld; g.bs = bs;                                                    \
+    return hsweep_launch<T, 0>(g, nlayers, B, (hipStream_t)stream);                                          \
+  }                                                                                                          \
+  extern "C" int fea_mg_hsweep_restrict_##SUF(const T* u, const T* u_raw, const T* f, T* out, T* fc,           \
+                                              const uint8_t* pid, const T* ktab, const T* omd, int ntab,       \
+                                              const T* hw, int nlayers, const T* rtab, int nrtab, T w0, int B,  \
+                                              int H, int W, int ld, long long bs, int ldc, long long bsc,       \
+                                              void* stream) {                                                  \
+    if (!f || !out || !fc || !ktab || !omd || !rtab || (!hw && nlayers > 0) || out == u || B <= 0 ||         \
+        B > 65535)                                                                                           \
+      return FEA_EINVAL;                                                                                     \
+    if (nlayers < 0 || nlayers > kHMaxLayers || !hs_layout_ok(H, W, ld, bs, sizeof(T)) || !(H & 1) || !(W & 1)) \
+      return FEA_EINVAL;                                                                                     \
+    const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;                                                            \
+    if (!hs_layout_ok(Hc, Wc, ldc, bsc, sizeof(T))) return FEA_EINVAL;                                        \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid) || (nrtab != ntab && nrtab != 1) ||        \
+        (ntab > 1 && nrtab == 1))                                                                            \
+      return FEA_EINVAL;                                                                                     \
+    if (u_raw && !u) return FEA_EINVAL;                                                                      \
+    HSArgs<T> g{};                                                                                           \
+    g.u = u; g.u_raw = u_raw; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.hw = hw;       \
+    g.ntab = ntab; g.H = H; g.W = W; g.ld = ld; g.bs = bs;                                                    \
+    g.fc = fc; g.rtab = rtab; g.w0 = w0; g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;                      \
+    return hsweep_launch<T, 2>(g, nlayers, B, (hipStream_t)stream);                                          \
+  }                                                                                                          \
+  extern "C" int fea_mg_prolong_hsweep_##SUF(const T* u, const T* u_raw, const T* ec, const T* f, T* out,       \
+                                             const uint8_t* pid,                                               \
+                                             const uint8_t* pidc, const T* ktab, const T* omd, int ntab,        \
+                                             const T* hw, int nlayers, const T* ptab, int nptab, T w1, int B,   \
+                                             int H, int W, int ld, long long bs, int ldc, long long bsc,        \
+                                             void* stream) {                                                   \
+    if (!u || !ec || !f || !out || !ktab || !omd || !ptab || (!hw && nlayers > 0) || out == u || B <= 0 ||   \
+        B > 65535)                                                                                           \
+      return FEA_EINVAL;                                                                                     \
+    if (nlayers < 0 || nlayers > kHMaxLayers || !hs_layout_ok(H, W, ld, bs, sizeof(T)) || !(H & 1) || !(W & 1)) \
+      return FEA_EINVAL;                                                                                     \
+    const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;                                                            \
+    if (!hs_layout_ok(Hc, Wc, ldc, bsc, sizeof(T))) return FEA_EINVAL;                                        \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (nptab != ntab && nptab != 1) ||                              \
+        (ntab > 1 && (!pid || !pidc || nptab == 1)))                                                          \
+      return FEA_EINVAL;                                                                                     \
+    HSArgs<T> g{};                                                                                           \
+    g.u = u; g.u_raw = u_raw; g.f = f; g.out = out; g.pid = pid; g.ktab = ktab; g.omd = omd; g.hw = hw;       \
+    g.ntab = ntab; g.H = H; g.W = W; g.ld = ld; g.bs = bs;                                                    \
+    g.ec = ec; g.pidc = pidc; g.ptab = ptab; g.w1 = w1; g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;       \
+    return hsweep_launch<T, 1>(g, nlayers, B, (hipStream_t)stream);                                          \
   }
 
 FEA_HNET_API(f32, float)

@@ -49,8 +49,12 @@ _SIGS = {
     "mg_prolong_add": [P, P, P, P, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_residual_norm": [P, P, P, P, I, P, P, I, I, I, I, LL, I, I, I, I, P],
     "mg_cycle_join": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", "S", I, I, I, I, LL, I, LL, P, P, P, P],
+    "mg_cycle_join_rects": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", "S", I, I, I, I, LL, I, LL, I, P, P],
     "mg_hsweep": [P, P, P, P, P, P, P, I, P, I, I, I, I, I, LL, P],
+    "mg_hsweep_restrict": [P, P, P, P, P, P, P, P, I, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
+    "mg_prolong_hsweep": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_coarse_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
+    "mg_hjac_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, P, I, "S", "S", I, I, I, P],
     # several coarse levels per launch (pointer arrays: ptr_array())
     "mg_mid_down": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
     "mg_mid_up": [P, P, P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
@@ -62,6 +66,7 @@ _EXTRA = {
     "fea_mg_join_norm_parts": ([I, I, I, I], LL),
     "fea_norm_append": ([P, LL, LL, I, I, P, P, P], I),
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
+    "fea_mg_hjac_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
     "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
     "fea_interface_pattern_map": ([P, LL, I, I, F64, P], I),
     "fea_dd_copy_blocks": ([P, I, I, I, P], I),
@@ -143,6 +148,10 @@ TAIL_LDS_LIMIT = 160 * 1024 - 1024
 
 def coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, multi):
     return int(lib().fea_mg_coarse_tail_lds_bytes(Ht, Wt, nlev, elem_size, int(bool(multi))))
+
+
+def hjac_tail_lds_bytes(Ht, Wt, nlev, elem_size, multi):
+    return int(lib().fea_mg_hjac_tail_lds_bytes(Ht, Wt, nlev, elem_size, int(bool(multi))))
 
 
 def weight_grad_ws_bytes(C, B, Hc, Wc):

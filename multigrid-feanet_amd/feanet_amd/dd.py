@@ -33,6 +33,8 @@ regions of one exchange are packed into one staging buffer by one kernel (fea_dd
 message per neighbour and unpacked by one kernel (row slabs: contiguous rows, sent in place).  D0 and D1 are the
 smallest depths for which the validity simulation keeps every owned node exact.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -410,6 +412,7 @@ class DDSolver:
         self.coarse_plan, self.coarse_end = self.coarse._build("a")
         assert self.joinable() == _joined(nu1, nu2, fuse)
         self.use_graph = graph
+        self._capture_ok = True
         self._segs = {}
         self._graphs = {}
         self._state = "a"
@@ -721,10 +724,61 @@ class DDSolver:
         return out
 
     # ------------------------------------------------------------------ driver (one process per rank)
+    GRAPH_CYCLES = 16  # joined cycles per captured graph (capturable communicators)
+
     def vcycle(self, k=1):
         if self.comm is None:
             raise RuntimeError("DDSolver.vcycle: no communicator (use LocalGroup for in-process ranks)")
         keys, end = self.program(k)
+        if self.use_graph and getattr(self.comm, "capturable", False) and self._capture_ok:
+            self._vcycle_captured(keys)
+        else:
+            self._run_chunks(keys, captured=False)
+        self._state = end
+
+    def _vcycle_captured(self, keys):
+        """vcycle with every chunk's kernels AND communication steps captured in one HIP graph per block of up to
+        GRAPH_CYCLES consecutive cycle joins (head and tail chunks: one graph each): a cycle costs no graph-launch
+        gaps between its kernel segments and ~one host graph launch per block.  Each block runs eagerly once
+        (plans, communicator set-up), is captured the second time and replayed after that.  A communicator whose
+        operations cannot be captured (capture raises) turns this off for the solver; it then runs the
+        segment-wise path."""
+        i = 0
+        while i < len(keys):
+            key = keys[i]
+            n = 1
+            if key[0] == "join":
+                while i + n < len(keys) and keys[i + n][0] == "join" and n < self.GRAPH_CYCLES:
+                    n += 1
+            block = keys[i:i + n]
+            gkey = ("cap",) + tuple(block)
+            g = self._graphs.get(gkey)
+            if g is None and gkey not in self._graphs:
+                self._graphs[gkey] = None  # eager once
+                self._run_chunks(block, captured=False)
+            elif g is None:
+                stream = torch.cuda.current_stream(self.device)
+                g = torch.cuda.CUDAGraph()
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(stream)
+                try:
+                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                        self._run_chunks(block, captured=True)
+                except RuntimeError:  # capture refused: this rank runs the segment-wise path from now on
+                    torch.cuda.synchronize(self.device)
+                    self._capture_ok = False
+                    self._run_chunks(keys[i:], captured=False)
+                    return
+                stream.wait_stream(s)
+                self._graphs[gkey] = g
+                g.replay()
+            else:
+                g.replay()
+            i += n
+
+    def _run_chunks(self, keys, captured=False):
+        """Issue the chunks' kernel segments and communication steps in order on the current stream; captured:
+        inside a graph capture (kernel segments launched directly, the level-0 halo completed within the block)."""
         pending = None  # level-0 halo exchange in flight (overlaps the coarse levels' kernels)
         for key in keys:
             segs, _ = self.chunk(key)
@@ -733,7 +787,10 @@ class DDSolver:
                     if lvl0 and pending is not None:
                         self.comm.exchange_finish(pending)
                         pending = None
-                    self.run_kernels(key, i)
+                    if captured:
+                        _launch_list(segs[i][1], self.dtype, torch.cuda.current_stream(self.device))
+                    else:
+                        self.run_kernels(key, i)
                 elif st[0] == "exchanges":
                     # coarse-level halos first (the next kernel needs them), the finest iterate's
                     # halo after, not waited for until a level-0 kernel runs: on RCCL both go out on
@@ -754,7 +811,6 @@ class DDSolver:
                     self.scatter(st[1])
         if pending is not None:
             self.comm.exchange_finish(pending)
-        self._state = end
 
     def residual_norm(self):
         n2 = self.residual_norm_sq_local()
@@ -837,7 +893,7 @@ class TorchComm:
     """Halo exchange / all-gather / all-reduce over torch.distributed.  With the nccl backend (RCCL
     on ROCm) device buffers are sent directly; with gloo they are staged through host memory."""
 
-    def __init__(self, group=None, dist=None):
+    def __init__(self, group=None, dist=None, capture=None):
         if dist is None:  # (tests pass an in-process stand-in with the same interface)
             import torch.distributed as dist
         self.dist = dist
@@ -845,6 +901,10 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.gpu = dist.get_backend(group) == "nccl"
+        # DDSolver captures whole cycles (kernels + RCCL calls) in HIP graphs only where asked: RCCL calls are
+        # stream-capturable, but a multi-rank capture cannot be rehearsed on one GPU (FEANET_DD_CAPTURE=1)
+        self.capturable = self.gpu and capture if capture is not None else (
+            self.gpu and os.environ.get("FEANET_DD_CAPTURE", "0") == "1")
 
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])

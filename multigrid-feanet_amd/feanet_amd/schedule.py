@@ -136,15 +136,21 @@ def vcycle_schedule(L, nu1=1, nu2=1, compat=None, start="a", tail_from=None, fus
     return steps, cur[0]
 
 
-def hjac_schedule(L, nu1=1, nu2=1, start="a"):
+def hjac_schedule(L, nu1=1, nu2=1, start="a", tail_from=None, fuse=False):
     """V-cycle of M-FEANet-mg_test.ipynb MultiGrid.Step with mode='hjac' (:27346-27372 with Relax =
     HJacIterator.HRelax, :147-155): every relaxation is one learned-smoother sweep ("hsweep", l, src,
     dst; src None = zero guess), so nothing is fused with the transfers:
     residual + restriction ("resid_restrict" with the current iterate) and prolongation + correction
     ("prolong_add") run as their own kernels; coarse levels start from zero, the coarsest gets
-    nu1 + nu2 sweeps."""
+    nu1 + nu2 sweeps.  tail_from = t (1 <= t < L): levels t .. L-1 run as ONE ("hjac_tail", t, dst) step
+    (fea_mg_hjac_tail, bitwise the steps it replaces) that reads f_t and writes level t's corrected iterate.
+    fuse: a level's last pre-sweep runs with its residual + restriction ("hsweep_restrict", l, src, dst) and its
+    prolongation + correction with the first post-sweep ("prolong_hsweep", l, u, e, dst; the corrected iterate
+    is never stored) — fea_mg_hsweep_restrict / fea_mg_prolong_hsweep, bitwise the pairs they replace."""
     if L < 1 or nu1 < 0 or nu2 < 0:
         raise ValueError("hjac_schedule: need L >= 1, nu1, nu2 >= 0")
+    if tail_from is not None and not 1 <= tail_from < L:
+        raise ValueError(f"hjac_schedule: tail_from={tail_from} outside [1, {L - 1}]")
     steps = []
     cur = ["zero"] * L
     cur[0] = start
@@ -158,17 +164,34 @@ def hjac_schedule(L, nu1=1, nu2=1, start="a"):
         for _ in range(nu1 + nu2):
             hs(0)
         return steps, cur[0]
-    for _ in range(nu1):
-        hs(0)
-    for l in range(L - 1):
+    top = L - 1 if tail_from is None else tail_from  # first level not streamed level by level
+
+    def pre_restrict(l):  # nu1 pre-sweeps of level l, then its residual + restriction
+        for i in range(nu1):
+            if fuse and i == nu1 - 1:
+                dst = "a" if cur[l] == "zero" else _other(cur[l])
+                steps.append(("hsweep_restrict", l, None if cur[l] == "zero" else cur[l], dst))
+                cur[l] = dst
+                return
+            hs(l)
         steps.append(("resid_restrict", l, cur[l], None))
-        if l + 1 < L - 1:
-            for _ in range(nu1):
-                hs(l + 1)
-    for _ in range(nu1 + nu2):
-        hs(L - 1)
-    for l in range(L - 2, -1, -1):
+
+    for l in range(top):
+        pre_restrict(l)
+    if tail_from is None:
+        for _ in range(nu1 + nu2):
+            hs(L - 1)
+    else:
+        steps.append(("hjac_tail", tail_from, "a"))
+        cur[tail_from] = "a"
+    for l in range(top - 1, -1, -1):
         dst = "a" if cur[l] == "zero" else _other(cur[l])
+        if fuse and nu2 >= 1:
+            steps.append(("prolong_hsweep", l, cur[l], cur[l + 1], dst))
+            cur[l] = dst
+            for _ in range(nu2 - 1):
+                hs(l)
+            continue
         steps.append(("prolong_add", l, cur[l], cur[l + 1], dst))
         cur[l] = dst
         for _ in range(nu2):

@@ -113,7 +113,8 @@ class MultigridSolver:
         smoother: "jac" (weighted Jacobi) or "hjac" (the learned smoother of M-FEANet-mg_test.ipynb,
             HJacIterator.HRelax: Jacobi + HNet correction; `hnet` = its [nl, 3, 3] conv weights, e.g.
             feanet_amd/weights/hnet_iso_poisson_33x33.npz).  "hjac" runs fea_mg_hsweep for every
-            relaxation (MultiGrid(mode='hjac').Step semantics) and no coarse tail.
+            relaxation (MultiGrid(mode='hjac').Step semantics); with coarse_tail its levels of <= 65^2 nodes
+            that fit in LDS run as one fea_mg_hjac_tail launch.
         join_cycles: vcycle(k) with k >= 2 runs the finest level's post-smooth of each cycle and the
             pre-smooth + residual + restriction of the next as one pass (fea_mg_cycle_join; bitwise
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
@@ -176,6 +177,8 @@ class MultigridSolver:
             hw = np.asarray(torch.as_tensor(hnet).detach().cpu().float().numpy(), np.float32).reshape(-1, 3, 3)
             if not 1 <= hw.shape[0] <= 3:
                 raise ValueError("MultigridSolver: HNet with 1..3 conv layers supported")
+        hjac_tail = coarse_tail and smoother == "hjac"
+        if smoother == "hjac":
             coarse_tail = False
         npdt = np.float32 if dtype == torch.float32 else np.float64
         multi = problem == "interface"
@@ -223,9 +226,20 @@ class MultigridSolver:
                         and 0 < _lib.coarse_tail_lds_bytes(Lv.H, Lv.W, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT):
                     self.tail_from = l
                     break
-        if self.tail_from is not None and multi:
+        # learned smoother: the levels of <= 65^2 nodes whose f, u and two scratch fields fit in LDS
+        self.hjac_tail_from = None
+        if hjac_tail:
+            esz = 4 if dtype == torch.float32 else 8
+            for l in range(1, self.L):
+                Lv = self.levels[l]
+                if (Lv.H <= 65 and Lv.W <= 65
+                        and 0 < _lib.hjac_tail_lds_bytes(Lv.H, Lv.W, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT):
+                    self.hjac_tail_from = l
+                    break
+        t_from = self.tail_from if self.tail_from is not None else self.hjac_tail_from
+        if t_from is not None and multi:
             maps = [ms.interface_pattern_map(self.levels[l].N, shape, size).reshape(-1)
-                    for l in range(self.tail_from, self.L)]
+                    for l in range(t_from, self.L)]
             self.tail_pid = torch.from_numpy(np.concatenate(maps)).to(dev)
         else:
             self.tail_pid = None
@@ -390,7 +404,8 @@ class MultigridSolver:
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
         if self.smoother == "hjac":
-            steps, end = hjac_schedule(self.L, self.nu1, self.nu2, start)
+            steps, end = hjac_schedule(self.L, self.nu1, self.nu2, start, tail_from=self.hjac_tail_from,
+                                       fuse=self.fuse)
         else:
             steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
                                          top_zero=self.zero_start)
@@ -508,6 +523,20 @@ class MultigridSolver:
                                        lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
                                        kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
                                        int(self.compat == "mm_interface_q2"), lv[t].B))
+        if kind == "hsweep_restrict":
+            return ("mg_hsweep_restrict", (ptr(l, st[2]), None, f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l), kt,
+                                           om, nt, self.hw.data_ptr(), self.nl, rt, nr, self.w[0]) + geom(l) +
+                    cgeom(l))
+        if kind == "prolong_hsweep":
+            return ("mg_prolong_hsweep", (ptr(l, st[2]), None, ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l), pid(l + 1), kt,
+                                          om, nt, self.hw.data_ptr(), self.nl, pt, npt, self.w[1]) + geom(l) +
+                    cgeom(l))
+        if kind == "hjac_tail":
+            t = l
+            return ("mg_hjac_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
+                                     lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
+                                     kt, om, nt, rt, pt, self.hw.data_ptr(), self.nl, self.w[0], self.w[1],
+                                     self.nu1, self.nu2, lv[t].B))
         raise ValueError(f"MultigridSolver: unknown schedule step {kind!r}")
 
     def _plan(self, start):
@@ -695,8 +724,11 @@ class MultigridSolver:
             if getattr(self, "_hjac_first", False):
                 self._hjac_first = False
                 first = list(plan)
+                # the first finest-level sweep of the cycle (its f is level 0's), whatever precedes it
+                f0 = self.levels[0].f.data_ptr()
                 for i, (name, args) in enumerate(first):
-                    if name == "mg_hsweep" and args[0] == self._ptr(0, self._state):
+                    fi = {"mg_hsweep": 2, "mg_hsweep_restrict": 2, "mg_prolong_hsweep": 3}.get(name)  # f's slot
+                    if fi is not None and args[fi] == f0:
                         first[i] = (name, (args[0], self._raw.data_ptr()) + args[2:])
                         break
                 self._launch(first)
@@ -955,7 +987,20 @@ class MultigridSolver:
         pb = 1 if self.problem == "interface" else 0
         total = 0
         for name, args in plan:
-            if name == "mg_coarse_tail":
+            if name in ("mg_coarse_tail", "mg_hjac_tail"):
+                continue
+            if name == "mg_hsweep":  # read u (NULL: zero guess) and f (+ pattern), write out
+                B, H, W = args[-5:-2]
+                total += B * (H - 2) * (W - 2) * (esz * (3 if args[0] is not None else 2) + pb)
+                continue
+            if name in ("mg_hsweep_restrict", "mg_prolong_hsweep"):  # (..., B, H, W, ld, bs, ldc, bsc)
+                B, H, W = args[-7:-4]
+                nodes = B * (H - 2) * (W - 2)
+                coarse = B * ((H + 1) // 2 - 2) * ((W + 1) // 2 - 2)
+                if name == "mg_hsweep_restrict":  # read u (or not), f; write out, f_c
+                    total += nodes * (esz * (3 if args[0] is not None else 2) + pb) + coarse * esz
+                else:  # read u, f, e; write out
+                    total += nodes * (3 * esz + pb) + coarse * (esz + pb)
                 continue
             if name in ("mg_mid_down", "mg_mid_up"):
                 k, B, H, W = args[4:8] if name == "mg_mid_up" else args[2:6]

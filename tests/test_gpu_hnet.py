@@ -123,3 +123,196 @@ def test_hjac_vcycle_vs_oracle(T):
         if T == torch.float64 or k == 0:
             err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
             assert err < (1e-10 if T == torch.float64 else 5e-5), (k, err)
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n", [("poisson", 1024), ("poisson", 2048), ("interface", 1024)])
+def test_hsweep_vs_oracle_large(T, problem, n):
+    """fea_mg_hsweep at the sizes the 4097^2 V-cycle's top levels run (1025^2, 2049^2), whose strip / task geometry
+    (rows per task adapted to the level, 17-36 strips) the small cases above do not reach: against the oracle's
+    HRelax, one sweep from a random iterate and one from the zero guess.  Two-material maps from the oracle's own
+    element/node loop (tests/golden/c3_pattern_maps.npz)."""
+    import os
+    from feanet_amd import _lib, mesh_setup as ms
+    from feanet_amd.solver import _Level
+    rng = np.random.default_rng(n + (problem == "interface"))
+    H = W = n + 1
+    pids = None
+    if problem == "interface":
+        maps = np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_pattern_maps.npz"))
+        pids = {H: maps[f"pid_{H}"]}
+        pid = pids[H]
+        assert np.array_equal(pid, ms.interface_pattern_map(H))
+    L = _Level(n, n, 1, T, torch.device("cuda"), pid if problem == "interface" else None)
+    ktab = ms.stencil_table((1, 20) if problem == "interface" else None)
+    omd = ms.omega_over_d(ktab, 2 / 3., npdt(T))
+    hw = (0.3 * rng.standard_normal((3, 3, 3))).astype(np.float32)
+    geo, _ = orc.square_geometry((H, W), npdt(T))
+    lvl = orc.Level(n, problem, npdt(T), pids=pids)
+    cu = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda().to(T)
+    kt, om, hwt = cu(ktab.reshape(-1, 9)), cu(omd), cu(hw.reshape(-1))
+    f = rng.standard_normal((1, H, W)).astype(npdt(T))
+    L.view(L.f).copy_(torch.from_numpy(f))
+    for zero in (False, True):
+        u = np.zeros((1, H, W), npdt(T)) if zero else rng.standard_normal((1, H, W)).astype(npdt(T))
+        L.view(L.a).copy_(torch.from_numpy(u))
+        L.view(L.b).fill_(7.0)
+        _lib.call("mg_hsweep", T, None if zero else L.a.data_ptr(), None, L.f.data_ptr(), L.b.data_ptr(),
+                  None if L.pid is None else L.pid.data_ptr(), kt.data_ptr(), om.data_ptr(), ktab.shape[0],
+                  hwt.data_ptr(), 3, *L.geom(), None)
+        out = L.view(L.b).cpu().numpy()
+        lvl.bc = u * (1 - geo)
+        ref = orc.hnet_relax(u, f, lvl, hw, 1)
+        err = np.abs(out[:, 1:-1, 1:-1] - ref[:, 1:-1, 1:-1]).max() / max(1.0, np.abs(ref).max())
+        assert err < TOL[T], (zero, err)
+        assert (out[:, 0] == 7).all() and (out[:, -1] == 7).all() and (out[:, :, 0] == 7).all()
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n,B,nl,nu", [("poisson", 32, 2, 3, (1, 1)), ("poisson", 128, 1, 3, (1, 1)),
+                                               ("poisson", 256, 1, 2, (2, 1)), ("poisson", 64, 3, 1, (1, 2)),
+                                               ("interface", 64, 2, 3, (1, 1)), ("interface", 128, 1, 3, (1, 1)),
+                                               ("poisson", 128, 1, 3, (0, 1))])
+def test_hjac_tail_bitwise(T, problem, n, B, nl, nu):
+    """fea_mg_hjac_tail (the learned-smoother V-cycle's coarse levels in one LDS-resident launch) is bitwise the
+    per-level fea_mg_hsweep / fea_mg_residual_restrict / fea_mg_prolong_add sequence it replaces: whole V-cycles
+    with and without it, both problems, batches, 1-3 HNet layers, V(1,1), V(2,1), V(1,2), V(0,1)."""
+    from feanet_amd.solver import MultigridSolver
+    rng = np.random.default_rng(n + B + nl)
+    hw = (0.25 * rng.standard_normal((nl, 3, 3))).astype(np.float32)
+    f = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).to("cuda", T)
+    out = []
+    for tail in (True, False):
+        s = MultigridSolver(n, dtype=T, batch=B, smoother="hjac", hnet=hw, problem=problem, nu1=nu[0], nu2=nu[1],
+                            coarse_tail=tail)
+        names = [name for name, _ in s._plan("a")[0]]
+        assert ("mg_hjac_tail" in names) == tail, names
+        if tail:  # the largest level <= 65^2 whose fields fit in LDS: 65^2 in fp32, 33^2 in fp64
+            top = 65 if T == torch.float32 else 33
+            t = s.hjac_tail_from
+            assert s.levels[t].H <= top and (t == 1 or s.levels[t - 1].H > top), (t, s.levels[t].H)
+        s.set_rhs(f=f)
+        s.load()
+        sols = []
+        for _ in range(3):
+            s.vcycle()
+            sols.append(s.solution())
+        out.append(sols)
+    for k, (a, b) in enumerate(zip(*out)):
+        assert torch.equal(a, b), (k, (a - b).abs().max().item())
+
+
+def _tables(problem, T, rng):
+    from feanet_amd import mesh_setup as ms
+    ktab = ms.stencil_table((1, 20) if problem == "interface" else None)
+    nt = ktab.shape[0]
+    cu = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda().to(T)
+    R = (rng.uniform(0.1, 0.4, (nt, 3, 3))).astype(np.float32)
+    P = (rng.uniform(0.1, 0.4, (nt, 3, 3))).astype(np.float32)
+    return (cu(ktab.reshape(-1, 9)), cu(ms.omega_over_d(ktab, 2 / 3., npdt(T))), nt, cu(R.reshape(-1, 9)),
+            cu(P.reshape(-1, 9)))
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,m,n,B", [("poisson", 8, 8, 1), ("poisson", 64, 64, 2), ("poisson", 300, 130, 1),
+                                           ("poisson", 16, 256, 1), ("poisson", 1024, 1024, 1),
+                                           ("interface", 32, 32, 3), ("interface", 256, 256, 1)])
+@pytest.mark.parametrize("nl", [3, 1])
+def test_hsweep_fused_kernels_bitwise(T, problem, m, n, B, nl):
+    """fea_mg_hsweep_restrict is bitwise fea_mg_hsweep then fea_mg_residual_restrict (stored iterate), from a
+    random iterate, the zero guess and with u_raw; fea_mg_prolong_hsweep is bitwise fea_mg_prolong_add then
+    fea_mg_hsweep.  Sizes cover strip and task edges, rows != columns, batches, both problems (per-pattern R/P);
+    boundary nodes of every output stay untouched."""
+    from feanet_amd import _lib, mesh_setup as ms
+    from feanet_amd.solver import _Level
+    if problem == "interface" and m != n:
+        pytest.skip("two-material problem is square")
+    rng = np.random.default_rng(m + 3 * n + B + nl)
+    pid = ms.interface_pattern_map(m + 1) if problem == "interface" else None
+    pidc = ms.interface_pattern_map(m // 2 + 1) if problem == "interface" else None
+    fr = _Level(m, n, B, T, torch.device("cuda"), pid)
+    cr = _Level(m // 2, n // 2, B, T, torch.device("cuda"), pidc)
+    kt, om, nt, rt, pt = _tables(problem, T, rng)
+    hw = torch.from_numpy((0.25 * rng.standard_normal((nl, 3, 3))).astype(np.float32).reshape(-1)).cuda().to(T)
+    H, W = m + 1, n + 1
+    put = lambda L, buf, x: L.view(L.buf(buf)).copy_(torch.from_numpy(x).to(T))
+    get = lambda L, buf: L.view(L.buf(buf)).clone()
+    fpid = None if fr.pid is None else fr.pid.data_ptr()
+    cpid = None if cr.pid is None else cr.pid.data_ptr()
+    put(fr, "f", rng.standard_normal((B, H, W)))
+    u = rng.standard_normal((B, H, W))
+    put(fr, "a", u)
+    put(fr, "zero", rng.standard_normal((B, H, W)))  # used as u_raw below
+    hs = (kt.data_ptr(), om.data_ptr(), nt, hw.data_ptr(), nl)
+    for variant in ("u", "zero", "raw"):
+        uptr = None if variant == "zero" else fr.a.data_ptr()
+        raw = fr.buf("zero").data_ptr() if variant == "raw" else None
+        # the output buffer's boundary holds the iterate's (Dirichlet) values, as both of the solver's ping-pong
+        # buffers do: the separate restriction reads them there (zero guess: a coarse level's zero boundary)
+        base = np.zeros((B, H, W)) if variant == "zero" else u
+        put(fr, "b", base)
+        put(cr, "f", np.full((B, cr.H, cr.W), 5.0))
+        _lib.call("mg_hsweep", T, uptr, raw, fr.f.data_ptr(), fr.b.data_ptr(), fpid, *hs, *fr.geom(), None)
+        _lib.call("mg_residual_restrict", T, fr.b.data_ptr(), fr.f.data_ptr(), None, cr.f.data_ptr(), fpid,
+                  kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), nt, 1.25, *fr.geom(), cr.ld, cr.bs, None)
+        ref_o, ref_c = get(fr, "b"), get(cr, "f")
+        put(fr, "b", base)
+        put(cr, "f", np.full((B, cr.H, cr.W), 5.0))
+        _lib.call("mg_hsweep_restrict", T, uptr, raw, fr.f.data_ptr(), fr.b.data_ptr(), cr.f.data_ptr(), fpid, *hs,
+                  rt.data_ptr(), nt, 1.25, *fr.geom(), cr.ld, cr.bs, None)
+        got_o, got_c = get(fr, "b"), get(cr, "f")
+        assert torch.equal(got_o, ref_o), (variant, (got_o - ref_o).abs().max().item())
+        assert torch.equal(got_c, ref_c), (variant, torch.nonzero(got_c != ref_c)[:5])
+        bt = torch.from_numpy(base).to("cuda", T)
+        assert torch.equal(got_o[:, 0], bt[:, 0]) and torch.equal(got_o[:, :, -1], bt[:, :, -1])
+        assert (got_c[:, 0] == 5).all() and (got_c[:, :, -1] == 5).all()
+    # prolongation + correction + sweep
+    e = rng.standard_normal((B, cr.H, cr.W))
+    e[:, 0] = e[:, -1] = e[:, :, 0] = e[:, :, -1] = 0
+    put(cr, "a", e)
+    put(fr, "b", np.full((B, H, W), 7.0))
+    put(fr, "c", u)  # prolong_add writes the interior: the boundary keeps the iterate's values, as the solver's
+    #                  ping-pong buffers both hold the Dirichlet data there
+    pp = (pt.data_ptr(), nt, 0.75)
+    _lib.call("mg_prolong_add", T, fr.a.data_ptr(), cr.a.data_ptr(), fr.c.data_ptr(), cpid, *pp, *fr.geom(), cr.ld,
+              cr.bs, None)
+    for raw in (None, fr.buf("zero").data_ptr()):  # the first sweep after a load sees the un-reset guess
+        put(fr, "b", np.full((B, H, W), 7.0))
+        _lib.call("mg_hsweep", T, fr.c.data_ptr(), raw, fr.f.data_ptr(), fr.b.data_ptr(), fpid, *hs, *fr.geom(), None)
+        ref = get(fr, "b")
+        put(fr, "b", np.full((B, H, W), 7.0))
+        _lib.call("mg_prolong_hsweep", T, fr.a.data_ptr(), raw, cr.a.data_ptr(), fr.f.data_ptr(), fr.b.data_ptr(), fpid,
+                  cpid, *hs, *pp, *fr.geom(), cr.ld, cr.bs, None)
+        got = get(fr, "b")
+        assert torch.equal(got, ref), (raw, (got - ref).abs().max().item())
+    assert (got[:, 0] == 7).all() and (got[:, -1] == 7).all()
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,n,B,nu", [("poisson", 128, 2, (1, 1)), ("poisson", 512, 1, (2, 1)),
+                                            ("interface", 128, 1, (1, 1)), ("poisson", 64, 1, (0, 2)),
+                                            ("poisson", 256, 1, (1, 0))])
+def test_hjac_fused_schedule_bitwise(T, problem, n, B, nu):
+    """MultigridSolver(smoother="hjac") with the fused level pairs (fuse=True: fea_mg_hsweep_restrict,
+    fea_mg_prolong_hsweep) and the coarse tail is bitwise the unfused per-level schedule, first cycle (u_raw from
+    a guess with a non-Dirichlet boundary) included."""
+    from feanet_amd.solver import MultigridSolver
+    rng = np.random.default_rng(n + B)
+    hw = (0.25 * rng.standard_normal((3, 3, 3))).astype(np.float32)
+    f = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).to("cuda", T)
+    u0 = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).to("cuda", T)
+    out = []
+    for fused in (True, False):
+        s = MultigridSolver(n, dtype=T, batch=B, smoother="hjac", hnet=hw, problem=problem, nu1=nu[0], nu2=nu[1],
+                            fuse=fused, coarse_tail=fused)
+        kinds = {name for name, _ in s._plan("a")[0]}
+        assert ("mg_prolong_hsweep" in kinds) == (fused and nu[1] > 0), kinds
+        s.set_rhs(f=f)
+        s.load(u0)
+        sols = []
+        for _ in range(3):
+            s.vcycle()
+            sols.append(s.solution())
+        out.append(sols)
+    for k, (a, b) in enumerate(zip(*out)):
+        assert torch.equal(a, b), (k, (a - b).abs().max().item())

@@ -6,6 +6,8 @@ V-cycles are compared with the oracle's MultiGrid.Step and with the reference's 
 residual histories (golden fixtures); at the benchmark size 4097^2 fp64 the checks are
 size-independent properties (convergence factor, exact scaling, batch independence).
 Tolerances: fp64 1e-12, fp32 5e-6, relative to max(1, max|expected|)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -1140,3 +1142,55 @@ def test_prolong2_bitwise(T, problem, n, m, B):
     got = fr.get("b")
     assert np.array_equal(got, ref), f"{np.argwhere(got != ref)[:5]}"
     assert (got[:, 0, :] == 7).all() and (got[:, :, -1] == 7).all() and (got[:, -1, :] == 7).all()
+
+
+@pytest.mark.parametrize("T", [torch.float64, torch.float32])
+@pytest.mark.parametrize("m,n,B,problem,cut", [(1024, 1024, 1, "poisson", (9, 16, 17)),
+                                               (514, 258, 2, "poisson", (3, 4, 5)),
+                                               (2048, 1024, 1, "poisson", (33, 64, 65)),
+                                               (256, 256, 1, "interface", (5, 8, 9)), (64, 64, 2, "poisson", (1, 2, 1))])
+def test_cycle_join_rects_bitwise(T, m, n, B, problem, cut):
+    """fea_mg_cycle_join_rects (the join over rectangles: a domain-decomposed rank's four border strips in one
+    launch, then its interior in another) covering the grid is bitwise the whole-grid fea_mg_cycle_join, both
+    outputs; border strips of `cut` = (coarse rows, left fine columns (even), right fine columns (odd): rectangle
+    bounds are odd) and a one-rectangle whole-grid launch."""
+    from feanet_amd import _lib
+    fr = Frame(n, B, T, problem, m=m)
+    co = Frame(n // 2, B, T, problem, m=m // 2)
+    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned=(problem == "interface"))
+    nt = ktab.shape[0]
+    rng = np.random.default_rng(m + n + B)
+    u, f = rand_state(rng, B, (fr.H, fr.W), T)
+    e = rng.standard_normal((B, co.H, co.W)).astype(npdt(T))
+    e[:, 0] = e[:, -1] = e[:, :, 0] = e[:, :, -1] = 0
+    fr.put("a", u)
+    fr.put("f", f)
+    co.put("a", e)
+    head = (fr.L.a.data_ptr(), co.L.a.data_ptr(), fr.L.f.data_ptr())
+    tail = (fr.pid(), co.pid(), kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, rt.data_ptr(), nt, 0.75, 1.25,
+            *fr.args(), co.L.ld, co.L.bs)
+    sent_c = np.full((B, co.H, co.W), 3.0)
+
+    def run(rect_sets):
+        out = fr.L.a.clone()
+        co.put("f", sent_c)
+        for rects in rect_sets:
+            if rects is None:
+                _lib.call("mg_cycle_join", T, *head, out.data_ptr(), co.L.f.data_ptr(), *tail, None, None, None, None)
+            else:
+                arr = (ctypes.c_int * (4 * len(rects)))(*[x for r in rects for x in r])
+                _lib.call("mg_cycle_join_rects", T, *head, out.data_ptr(), co.L.f.data_ptr(), *tail, len(rects),
+                          ctypes.addressof(arr), None)
+        torch.cuda.synchronize()
+        return fr.L.view(out).clone(), co.get("f").copy()
+
+    Hc, W = co.H, fr.W
+    a, cl, cr = cut
+    border = [(1, 1 + a, 1, W - 1), (Hc - 1 - a, Hc - 1, 1, W - 1), (1 + a, Hc - 1 - a, 1, 1 + cl),
+              (1 + a, Hc - 1 - a, W - 1 - cr, W - 1)]
+    interior = [(1 + a, Hc - 1 - a, 1 + cl, W - 1 - cr)]
+    ref_u, ref_f = run([None])
+    for sets in ([border, interior], [interior, border], [[(1, Hc - 1, 1, W - 1)]]):
+        got_u, got_f = run(sets)
+        assert torch.equal(got_u, ref_u), (sets, (got_u - ref_u).abs().max().item())
+        assert np.array_equal(got_f, ref_f), sets

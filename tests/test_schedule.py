@@ -42,7 +42,17 @@ def interpret(mg, steps, v, f, compat=None):
             expanded.append(st)
     for st in expanded:
         kind, l = st[0], st[1]
-        if kind == "sweep":
+        if kind in ("hsweep", "hsweep_restrict"):  # learned-smoother sweep: the oracle's HRelax with mg.hw
+            src = np.zeros((B, lv[l].H, lv[l].W), dt) if st[2] is None else get(l, st[2])
+            bufs[l][st[3]] = orc.hnet_relax(src, fs[l], lv[l], mg.hw)
+            if kind == "hsweep_restrict":
+                fs[l + 1] = orc.restrict(fs[l] - lv[l].K(bufs[l][st[3]]), lv[l].pid, mg.rtab, mg.w[0])
+        elif kind == "prolong_hsweep":
+            x = get(l, st[2]) + orc.prolong(get(l + 1, st[3]), lv[l + 1].pid, mg.ptab, mg.w[1])
+            bufs[l][st[4]] = orc.hnet_relax(x, fs[l], lv[l], mg.hw)
+        elif kind == "hjac_tail":
+            bufs[l][st[2]] = hjac_tail_oracle(mg, l, fs[l], B)
+        elif kind == "sweep":
             src = np.zeros((B, lv[l].H, lv[l].W), dt) if st[2] is None else get(l, st[2])
             bufs[l][st[3]] = lv[l].sweep(src, fs[l])
         elif kind == "resid_restrict":
@@ -104,6 +114,58 @@ def tail_oracle(mg, t, f_t, compat, B, nu1=None, nu2=None, q2=None):
         for _ in range(nu2):
             v[k] = lv[k].sweep(v[k], f[k])
     return v[0]
+
+
+def hjac_tail_oracle(mg, t, f_t, B):
+    """The hjac_tail kernel's loop (hjac_tail.hip) restated with oracle ops (HRelax sweeps)."""
+    nu1, nu2 = mg.nu
+    lv = mg.levels[t:]
+    zeros = lambda k: np.zeros((B, lv[k].H, lv[k].W), mg.dtype)
+    f = [f_t] + [None] * (len(lv) - 1)
+    v = [zeros(k) for k in range(len(lv))]
+    for k in range(len(lv) - 1):
+        for _ in range(nu1):
+            v[k] = orc.hnet_relax(v[k], f[k], lv[k], mg.hw)
+        f[k + 1] = orc.restrict(f[k] - lv[k].K(v[k]), lv[k].pid, mg.rtab, mg.w[0])
+    k = len(lv) - 1
+    for _ in range(nu1 + nu2):
+        v[k] = orc.hnet_relax(v[k], f[k], lv[k], mg.hw)
+    for k in range(len(lv) - 2, -1, -1):
+        v[k] = v[k] + orc.prolong(v[k + 1], lv[k + 1].pid, mg.ptab, mg.w[1])
+        for _ in range(nu2):
+            v[k] = orc.hnet_relax(v[k], f[k], lv[k], mg.hw)
+    return v[0]
+
+
+@pytest.mark.parametrize("fuse", [False, True])
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("tail", [None, 1, 2, 4])
+def test_hjac_tail_schedule_equals_step(problem, tail, fuse):
+    """hjac_schedule (MultiGrid.Step mode='hjac', every relaxation one HRelax) with its coarse levels as one
+    "hjac_tail" step (tail_from) is the oracle's Step with every sweep replaced by HRelax."""
+    from feanet_amd.schedule import hjac_schedule
+    n, L = 32, 5
+    rng = np.random.default_rng(13)
+    for nu in ((1, 1), (2, 1), (1, 2), (0, 1)):
+        mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+        mg.nu, mg.hw = nu, 0.3 * rng.standard_normal((3, 3, 3))
+        v = rng.standard_normal((2, n + 1, n + 1))
+        f = rng.standard_normal((2, n + 1, n + 1))
+        steps, end = hjac_schedule(L, *nu, tail_from=tail, fuse=fuse)
+        assert sum(st[0] == "hjac_tail" for st in steps) == (tail is not None)
+        kinds = {st[0] for st in steps}
+        assert ("hsweep_restrict" in kinds) == (fuse and nu[0] > 0) and ("prolong_hsweep" in kinds) == fuse
+        for st in steps:  # a fused prolongation never writes the iterate it reads
+            assert st[0] != "prolong_hsweep" or st[2] != st[4]
+        out = interpret(mg, steps, v, f)[0][end]
+        ref_steps, ref_end = hjac_schedule(L, *nu)
+        ref = interpret(mg, ref_steps, v, f)[0][ref_end]
+        np.testing.assert_allclose(out, ref, rtol=1e-13, atol=1e-13)
+        if nu == (1, 1):  # and the reference's Step with HRelax sweeps
+            for lvl in mg.levels:
+                lvl.sweep = (lambda ll, o: (lambda x, ff: (lambda j: j + orc.hnet(j - x, ll.geo, mg.hw))(o(x, ff))))(
+                    lvl, lvl.sweep)
+            np.testing.assert_allclose(out, mg.step(v, f), rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.parametrize("problem", ["poisson", "interface"])

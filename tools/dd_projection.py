@@ -29,6 +29,7 @@ class NullComm:
     """A communicator that moves nothing: exchanges and the all-gather are no-ops, the all-reduce is the
     identity.  Only for timing one rank's kernels (values are not those of a real decomposition)."""
     gpu = True
+    capturable = True  # (--segments: False, the segment-wise path)
 
     def exchange_many(self, s, items, wait=True, packed=False):
         return None
@@ -112,6 +113,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-pack", action="store_true", help="leave out the halo pack / unpack kernels")
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly (no HIP graphs)")
+    ap.add_argument("--segments", action="store_true",
+                    help="one graph per kernel segment between communication steps (the path of communicators that "
+                         "cannot be captured) instead of whole captured cycles")
     ap.add_argument("--graph-min", type=int, default=None, help="DDSolver(graph_min=): shorter segments eager")
     args = ap.parse_args()
     n = args.n
@@ -135,7 +139,9 @@ def main():
         rec["ranks"][P] = {"grid": f"{Pr}x{Pc}", "rank": r, "default_ld": d, "ld": {}}
         for Ld in lds:
             try:
-                s = DDSolver(n, n, r, P, comm=NullComm() if args.no_pack else PackComm(), agglomerate=Ld, grid=(Pr, Pc),
+                comm = NullComm() if args.no_pack else PackComm()
+                comm.capturable = not args.segments
+                s = DDSolver(n, n, r, P, comm=comm, agglomerate=Ld, grid=(Pr, Pc),
                              graph=not args.no_graph,
                              **({} if args.graph_min is None else {"graph_min": args.graph_min}))
             except ValueError as e:
