@@ -327,7 +327,7 @@ int fea_mg_prolong_add_f64(const double* u, const double* ec, double* out, const
 
 /* The cycle join (fea_mg_cycle_join, no residual norm) over nrect <= 4 rectangles of the grid in one launch:
  * rects[4 r ..] = {I0, I1, c0, c1}: coarse rows [I0, I1) (their fine rows 2I-1, 2I; row H-2 with I1 = Hc-1) and
- * fine columns [c0, c1), c0 and c1 odd (coarse column J with fine columns 2J-1, 2J).  Rectangles covering the
+ * fine columns [c0, c1), c0 odd, c1 odd or W-1 (coarse column J with fine columns 2J-1, 2J).  Rectangles covering the
  * grid give fea_mg_cycle_join's result bitwise; a domain-decomposed rank computes the border strips its halo
  * exchange sends first and the interior while the messages are in flight (feanet_amd.dd). */
 int fea_mg_cycle_join_rects_f32(const float* u, const float* ec, const float* f, float* u_out, float* fc,

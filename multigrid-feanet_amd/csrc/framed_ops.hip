@@ -23,6 +23,7 @@
 #include "fea_common.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace fea {
 
@@ -1873,20 +1874,19 @@ struct Ovl4 {
   static constexpr int S = 59 * V;      // owned fine columns per strip (fp64 118, fp32 236)
 };
 
-template <typename T, bool MULTI>
-__global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
+// PROLONG2 ALT: odd row tasks stream bottom-up (REV), so vertically adjacent tasks read the rows they share (the
+// fine halo row, the coarse stage's extra rows) at the same moment and the second read is an L2 hit.
+#ifndef FEA_PROLONG2_ALT
+#define FEA_PROLONG2_ALT 1
+#endif
+constexpr bool kProlong2Alternate = FEA_PROLONG2_ALT != 0;
+
+template <typename T, bool MULTI, bool REV>
+__device__ __forceinline__ void prolong2_task(const MgArgs<T>& g, const TaskId& id, const T* tab, const T* ptb) {
   using F = Frame<T>;
   using O = Ovl4<T>;
   constexpr int V = F::VEC;
   constexpr int Q = V / 2;
-  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
-  if constexpr (MULTI) {
-    load_tables<T>(tab, g.ktab, g.omd, g.ntab, ptb, g.ptab, g.nptab);
-    __syncthreads();
-  }
-  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
-  if (!id.valid) return;
   const int lane = lane_id();
   const int H = g.H, Hc = g.Hc, W = g.W, Wc = g.Wc, Hc2 = g.Hc2, Wc2 = g.Wc2;
   const int c0 = 1 + id.s * O::S;  // first owned fine column
@@ -2076,63 +2076,144 @@ __global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
     if (own) store_masked<T, V, false>(ob + rowo(y), o, cl, W);
   };
 
-  // coarse stage start: x' rows a0-1 .. a0+2 -> u' rows a0 (C0), a0+1 (C1)
-  const int a0 = (r0 - 1) / 2;
-  X2 Xa = mkx2(ld2(a0 - 1), a0 - 1);
-  X2 Xb = mkx2(ld2(a0), a0);
-  X2 Xc2 = mkx2(ld2(a0 + 1), a0 + 1);
-  const CRow<T, V> C0 = mku2(Xa, Xb, Xc2, a0);
-  Xa = Xb;
-  Xb = Xc2;
-  Xc2 = mkx2(ld2(a0 + 2), a0 + 2);
-  CRow<T, V> C1 = mku2(Xa, Xb, Xc2, a0 + 1);
-  XR Xp = row_even(ld_f(r0 - 1), r0 - 1, C0);
-  XR Xc = row_odd(ld_f(r0), r0, C0, C1);
-  // iteration y (odd) emits fine rows y, y+1 from fine rows y+1, y+2 and u' row (y+3)/2, which needs x' row
-  // (y+5)/2: those loads are in flight kProlongAhead iterations ahead (ring slots consumed in place)
-  constexpr int D = kProlongAhead;
-  struct Slot {
-    In u1, u2;
-    In2 c;
-  };
-  Slot ring[D];
-  auto fill = [&](Slot& sl, int y) {
-    sl.u1 = ld_f(y + 1);
-    sl.u2 = ld_f(y + 2);
-    sl.c = ld2((y + 5) / 2);
-  };
-#pragma unroll
-  for (int d = 0; d < D; ++d) fill(ring[d], r0 + 2 * d);
-  auto iter = [&](int y, auto slot) {
-    Slot& sl = ring[decltype(slot)::value];
-    const XR Xn = row_even(sl.u1, y + 1, C1);  // row y+1 (even, coarse (y+1)/2 = C1)
-    emit(y, Xp, Xc, Xn);
-    if (y + 1 < r1) {  // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
-      Xa = Xb;
-      Xb = Xc2;
-      Xc2 = mkx2(sl.c, (y + 5) / 2);
-      const CRow<T, V> C2 = mku2(Xa, Xb, Xc2, (y + 3) / 2);
-      const XR Xnn = row_odd(sl.u2, y + 2, C1, C2);
-      emit(y + 1, Xc, Xn, Xnn);
-      Xp = Xn;
-      Xc = Xnn;
-      C1 = C2;
+  if constexpr (!REV) {
+    // coarse stage start: x' rows a0-1 .. a0+2 -> u' rows a0 (C0), a0+1 (C1)
+    const int a0 = (r0 - 1) / 2;
+    X2 Xa = mkx2(ld2(a0 - 1), a0 - 1);
+    X2 Xb = mkx2(ld2(a0), a0);
+    X2 Xc2 = mkx2(ld2(a0 + 1), a0 + 1);
+    const CRow<T, V> C0 = mku2(Xa, Xb, Xc2, a0);
+    Xa = Xb;
+    Xb = Xc2;
+    Xc2 = mkx2(ld2(a0 + 2), a0 + 2);
+    CRow<T, V> C1 = mku2(Xa, Xb, Xc2, a0 + 1);
+    XR Xp = row_even(ld_f(r0 - 1), r0 - 1, C0);
+    XR Xc = row_odd(ld_f(r0), r0, C0, C1);
+    // iteration y (odd) emits fine rows y, y+1 from fine rows y+1, y+2 and u' row (y+3)/2, which needs x' row
+    // (y+5)/2: those loads are in flight kProlongAhead iterations ahead (ring slots consumed in place)
+    constexpr int D = kProlongAhead;
+    struct Slot {
+      In u1, u2;
+      In2 c;
+    };
+    Slot ring[D];
+    auto fill = [&](Slot& sl, int y) {
+      sl.u1 = ld_f(y + 1);
+      sl.u2 = ld_f(y + 2);
+      sl.c = ld2((y + 5) / 2);
+    };
+  #pragma unroll
+    for (int d = 0; d < D; ++d) fill(ring[d], r0 + 2 * d);
+    auto iter = [&](int y, auto slot) {
+      Slot& sl = ring[decltype(slot)::value];
+      const XR Xn = row_even(sl.u1, y + 1, C1);  // row y+1 (even, coarse (y+1)/2 = C1)
+      emit(y, Xp, Xc, Xn);
+      if (y + 1 < r1) {  // row y+2 (odd, coarse (y+1)/2 and (y+3)/2)
+        Xa = Xb;
+        Xb = Xc2;
+        Xc2 = mkx2(sl.c, (y + 5) / 2);
+        const CRow<T, V> C2 = mku2(Xa, Xb, Xc2, (y + 3) / 2);
+        const XR Xnn = row_odd(sl.u2, y + 2, C1, C2);
+        emit(y + 1, Xc, Xn, Xnn);
+        Xp = Xn;
+        Xc = Xnn;
+        C1 = C2;
+      }
+      fill(sl, y + 2 * D);
+    };
+    int y = r0;
+    for (; y + 2 * (D - 1) < r1; y += 2 * D) {
+      iter(y, std::integral_constant<int, 0>{});
+      if constexpr (D > 1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+      if constexpr (D > 2) iter(y + 4, std::integral_constant<int, 2 % D>{});
+      if constexpr (D > 3) iter(y + 6, std::integral_constant<int, 3 % D>{});
     }
-    fill(sl, y + 2 * D);
-  };
-  int y = r0;
-  for (; y + 2 * (D - 1) < r1; y += 2 * D) {
-    iter(y, std::integral_constant<int, 0>{});
-    if constexpr (D > 1) iter(y + 2, std::integral_constant<int, 1 % D>{});
-    if constexpr (D > 2) iter(y + 4, std::integral_constant<int, 2 % D>{});
-    if constexpr (D > 3) iter(y + 6, std::integral_constant<int, 3 % D>{});
+    if constexpr (D > 1)
+      if (y < r1) iter(y, std::integral_constant<int, 0>{});
+    if constexpr (D > 2)
+      if (y + 2 < r1) iter(y + 2, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 3)
+      if (y + 4 < r1) iter(y + 4, std::integral_constant<int, 2 % D>{});
+  } else {
+    // bottom-up: pairs of fine rows (y + 1 even, then y odd) for odd y from the last one down; entering the pair
+    // of y the window holds x(y + 2), x(y + 1), the coarse stage u'((y + 1) / 2) and x' rows (y+3)/2 .. (y-1)/2
+    const int yl = r1 - 1;
+    const int yt = (yl & 1) ? yl : yl - 1;  // first (bottom) pair
+    const int A = (yt + 1) / 2;
+    X2 Xa = mkx2(ld2(A + 2), A + 2);
+    X2 Xb = mkx2(ld2(A + 1), A + 1);
+    X2 Xc2 = mkx2(ld2(A), A);
+    const CRow<T, V> Chi1 = mku2(Xc2, Xb, Xa, A + 1);  // u'(A + 1)
+    Xa = Xb;
+    Xb = Xc2;
+    Xc2 = mkx2(ld2(A - 1), A - 1);
+    CRow<T, V> Chi = mku2(Xc2, Xb, Xa, A);  // u'(A)
+    XR R0 = row_odd(ld_f(yt + 2), yt + 2, Chi, Chi1);  // x(yt + 2)
+    XR R1 = row_even(ld_f(yt + 1), yt + 1, Chi);       // x(yt + 1)
+    // pair y's inputs (f rows y, y - 1 and the x' row (y - 3) / 2) in flight kProlongAhead pairs ahead
+    constexpr int D = kProlongAhead;
+    struct Slot {
+      In u1, u2;
+      In2 c;
+    };
+    Slot ring[D];
+    auto fill = [&](Slot& sl, int y) {
+      sl.u1 = ld_f(y);
+      sl.u2 = ld_f(y - 1);
+      sl.c = ld2((y - 3) / 2);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) fill(ring[d], yt - 2 * d);
+    auto iter = [&](int y, auto slot) {
+      Slot& sl = ring[decltype(slot)::value];
+      Xa = Xb;  // x' rows (y+1)/2, (y-1)/2, (y-3)/2 -> u'((y - 1) / 2)
+      Xb = Xc2;
+      Xc2 = mkx2(sl.c, (y - 3) / 2);
+      const CRow<T, V> Clo = mku2(Xc2, Xb, Xa, (y - 1) / 2);
+      const XR Xy = row_odd(sl.u1, y, Clo, Chi);  // x(y)
+      if (y + 1 < r1) emit(y + 1, Xy, R1, R0);
+      const XR Xm = row_even(sl.u2, y - 1, Clo);  // x(y - 1)
+      emit(y, Xm, Xy, R1);
+      R0 = Xy;
+      R1 = Xm;
+      Chi = Clo;
+      fill(sl, y - 2 * D);
+    };
+    int y = yt;
+    for (; y - 2 * (D - 1) >= r0; y -= 2 * D) {
+      iter(y, std::integral_constant<int, 0>{});
+      if constexpr (D > 1) iter(y - 2, std::integral_constant<int, 1 % D>{});
+      if constexpr (D > 2) iter(y - 4, std::integral_constant<int, 2 % D>{});
+      if constexpr (D > 3) iter(y - 6, std::integral_constant<int, 3 % D>{});
+    }
+    if constexpr (D > 1)
+      if (y >= r0) iter(y, std::integral_constant<int, 0>{});
+    if constexpr (D > 2)
+      if (y - 2 >= r0) iter(y - 2, std::integral_constant<int, 1 % D>{});
+    if constexpr (D > 3)
+      if (y - 4 >= r0) iter(y - 4, std::integral_constant<int, 2 % D>{});
   }
-  if constexpr (D > 1)
-    if (y < r1) iter(y, std::integral_constant<int, 0>{});
-  if constexpr (D > 2)
-    if (y + 2 < r1) iter(y + 2, std::integral_constant<int, 1 % D>{});
-  if constexpr (D > 3)
-    if (y + 4 < r1) iter(y + 4, std::integral_constant<int, 2 % D>{});
+}
+
+template <typename T, bool MULTI>
+__global__ __launch_bounds__(256) void k_mg_prolong2(MgArgs<T> g) {
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  __shared__ T ptb[MULTI ? FEA_MAX_PATTERNS * kTabStride : 1];
+  if constexpr (MULTI) {
+    load_tables<T>(tab, g.ktab, g.omd, g.ntab, ptb, g.ptab, g.nptab);
+    __syncthreads();
+  }
+  const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+  if (!id.valid) return;
+  // fp64 only: the reversed task body needs ~150 VGPRs (fp32 forward: 100, 4 waves per SIMD), which costs the
+  // batched fp32 cycles (C5: 52 instead of 42 us) more than the L2 reuse gains; fp64 gains 1 us at 4097^2
+  if constexpr (kProlong2Alternate && sizeof(T) == 8) {
+    if (id.t & 1) {
+      prolong2_task<T, MULTI, true>(g, id, tab, ptb);
+      return;
+    }
+  }
+  prolong2_task<T, MULTI, false>(g, id, tab, ptb);
 }
 
 // ---------------------------------------------------------------------------
@@ -2164,6 +2245,25 @@ __device__ __forceinline__ X& pick(X& a, X& b) {
 #define FEA_JOIN_WAVES 0
 #endif
 static_assert(FEA_JOIN_AHEAD == 2 || FEA_JOIN_AHEAD == 4, "join prefetch ring of 2 or 4 rows");
+#ifndef FEA_JOIN_UNROLL
+#define FEA_JOIN_UNROLL 4
+#endif
+constexpr int kJoinUnroll = FEA_JOIN_UNROLL;
+// FEA_JOIN_PEEL: fp32 joins peel the pipeline fill (compile-time stage flags); fp64 keeps runtime flags
+#ifndef FEA_JOIN_PEEL
+#define FEA_JOIN_PEEL 1
+#endif
+constexpr bool kJoinPeel = FEA_JOIN_PEEL != 0;
+static_assert(kJoinUnroll % FEA_JOIN_AHEAD == 0 && kJoinUnroll % 2 == 0, "join unroll: a multiple of the ring");
+// f(integral_constant<int, i>) for i = 0 .. N-1, in order (compile-time step positions)
+template <int N, typename Fn, int... I>
+__device__ __forceinline__ void unroll_steps_(Fn&& fn, std::integer_sequence<int, I...>) {
+  (fn(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void unroll_steps(Fn&& fn) {
+  unroll_steps_<N>(fn, std::make_integer_sequence<int, N>{});
+}
 // FEA_JOIN_NTL: nontemporal loads of the iterate u in the join on levels above the NT threshold
 #ifndef FEA_JOIN_NTL
 #define FEA_JOIN_NTL 1
@@ -2333,10 +2433,15 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
     else sweep_own(a, b, c, pa, pb_, pc, fy, keep, y, o, count);
   };
 
-  auto step = [&](int y, auto par) {
+  // nn: the step index where it is < kFill (the pipeline's fill steps run stages 2 .. 4 only from step 2, 4, 6
+  // on, and the first residual row closes no coarse row), kFill or more for every later step.  Peeled (fp32):
+  // a compile-time constant, so the steady-state steps carry no stage branches; fp64 passes the runtime step
+  // index (the peeled fp64 body needs 180 VGPRs, 2 waves per SIMD instead of 3: 16 us slower at 4097^2)
+  constexpr int kFill = 7;
+  auto step = [&](int y, auto par, auto nn) {
     constexpr int SLOT = decltype(par)::value % kJoinAhead;  // step index mod kJoinAhead
     constexpr int ODD = decltype(par)::value & 1;            // y odd (yb is even)
-    const int n = REV ? ye - y : y - ys;                     // step index
+    const int NN = nn;
     // this step's inputs; refill the slot with the rows kJoinAhead steps ahead
     T(&bu)[V] = ub_[SLOT];
     T(&bf)[V] = fb_[SLOT];
@@ -2380,14 +2485,14 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
     P1 = P0;
     if constexpr (MULTI) P0 = own_prow<T, V>(p0);
     // 2. v(y-s) = J(x) (boundary nodes keep u)
-    if (n >= 2) {
+    if (NN >= 2) {
       T v[V];
       sweep3(Xa, Xb, Xc, P2, P1, P0, fy1, um1, y - S, v, false);
       Va = Vb;
       Vb = Vc;
       Vc = own_row<T, V>(v);
       // 3. w(y-2s) = J(v) (boundary nodes keep v)
-      if (n >= 4) {
+      if (NN >= 4) {
         T keep[V], w[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) keep[k] = Vb.a[k + 1];
@@ -2399,7 +2504,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
         Wb = Wc_;
         Wc_ = own_row<T, V>(w);
         // 4. residual row y-3s -> restriction
-        if (n >= 6) {
+        if (NN >= 6) {
           T r[V + 1];
 #pragma unroll
           for (int k = 0; k < V; ++k) {
@@ -2435,7 +2540,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
           };
           if constexpr (!REV) {
             if constexpr (!ODD) {  // yr odd = 2I+1: ky = 2 closes coarse row I, ky = 0 opens I+1
-              if (yr > 2 * I0 - 1) {
+              if (NN > 6) {  // (yr > 2 I0 - 1)
                 T o[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) o[q] = w0 * (acc[q] + term(q, 2));
@@ -2449,7 +2554,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
             }
           } else {
             if constexpr (!ODD) {  // yr odd = 2I-1: ky = 0 closes coarse row I, ky = 2 opens I-1
-              if (yr < 2 * I1 - 1) {
+              if (NN > 6) {  // (yr < 2 I1 - 1)
                 T o[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) o[q] = w0 * ((term(q, 0) + acc[q]) + t2[q]);
@@ -2475,30 +2580,39 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
     }
   };
 
-  // ye - ys + 1 steps (odd); the ring slot is a template argument, so the loop is unrolled by 4 (a
-  // multiple of the ring)
-  if constexpr (!REV) {
-    int y = ys;
-    for (; y + 3 <= ye; y += 4) {
-      step(y, std::integral_constant<int, 0>{});
-      step(y + 1, std::integral_constant<int, 1>{});
-      step(y + 2, std::integral_constant<int, 2>{});
-      step(y + 3, std::integral_constant<int, 3>{});
+  // ye - ys + 1 steps (odd); the ring slot is a template argument, so the loop is unrolled by a multiple of
+  // the ring: FEA_JOIN_UNROLL = 4, or 6 (= the 3-row window period x the 2-slot ring: every window rotation
+  // is a register renaming inside the body and the loop's back edge needs no moves)
+  if constexpr (kJoinPeel && sizeof(T) == 4) {
+    constexpr int U = kJoinUnroll;
+    using Full = std::integral_constant<int, kFill>;
+    // the kFill fill steps (>= 9 steps per task: rb >= 2), then the steady state in blocks of U (the step
+    // index parity after the fill is kFill's: pass positions kFill .. kFill + U - 1 so slot and parity stay exact)
+    unroll_steps<kFill>([&](auto i) { step(REV ? ye - decltype(i)::value : ys + decltype(i)::value, i, i); });
+    int y = REV ? ye - kFill : ys + kFill;
+    if constexpr (!REV) {
+      for (; y + U - 1 <= ye; y += U)
+        unroll_steps<U>([&](auto i) { step(y + decltype(i)::value, std::integral_constant<int, kFill + decltype(i)::value>{}, Full{}); });
+      unroll_steps<U - 1>([&](auto i) {
+        if (y + decltype(i)::value <= ye)
+          step(y + decltype(i)::value, std::integral_constant<int, kFill + decltype(i)::value>{}, Full{});
+      });
+    } else {
+      for (; y - (U - 1) >= ys; y -= U)
+        unroll_steps<U>([&](auto i) { step(y - decltype(i)::value, std::integral_constant<int, kFill + decltype(i)::value>{}, Full{}); });
+      unroll_steps<U - 1>([&](auto i) {
+        if (y - decltype(i)::value >= ys)
+          step(y - decltype(i)::value, std::integral_constant<int, kFill + decltype(i)::value>{}, Full{});
+      });
     }
-    if (y <= ye) step(y, std::integral_constant<int, 0>{});
-    if (y + 1 <= ye) step(y + 1, std::integral_constant<int, 1>{});
-    if (y + 2 <= ye) step(y + 2, std::integral_constant<int, 2>{});
   } else {
-    int y = ye;
-    for (; y - 3 >= ys; y -= 4) {
-      step(y, std::integral_constant<int, 0>{});
-      step(y - 1, std::integral_constant<int, 1>{});
-      step(y - 2, std::integral_constant<int, 2>{});
-      step(y - 3, std::integral_constant<int, 3>{});
-    }
-    if (y >= ys) step(y, std::integral_constant<int, 0>{});
-    if (y - 1 >= ys) step(y - 1, std::integral_constant<int, 1>{});
-    if (y - 2 >= ys) step(y - 2, std::integral_constant<int, 2>{});
+    int y = yb;
+    for (; REV ? y - 3 >= ys : y + 3 <= ye; y += 4 * S)
+      unroll_steps<4>([&](auto i) { step(y + S * decltype(i)::value, i, S * (y - yb) + decltype(i)::value); });
+    unroll_steps<3>([&](auto i) {
+      if (REV ? y - decltype(i)::value >= ys : y + decltype(i)::value <= ye)
+        step(y + S * decltype(i)::value, i, S * (y - yb) + decltype(i)::value);
+    });
   }
 }
 
@@ -3093,7 +3207,7 @@ FEA_MG_API(f64, double)
 // The cycle join over up to four rectangles of the grid in ONE launch (a domain-decomposed rank's border strips,
 // whose nodes its halo exchange sends, ahead of the interior that runs while the messages are in flight).
 // rects: nrect x {I0, I1, c0, c1}: coarse rows [I0, I1) with their fine rows 2I-1, 2I (and row H-2 when I1 = Hc-1),
-// fine columns [c0, c1) with odd c0, c1 (coarse column J goes with fine columns 2J-1, 2J).  Every node is the same
+// fine columns [c0, c1) with odd c0 and c1 odd or W-1 (coarse column J goes with fine columns 2J-1, 2J).  Every node is the same
 // expression as in the whole-grid launch, so a cover of the grid by rectangles is bitwise fea_mg_cycle_join.
 template <typename T>
 static int cycle_join_rects(const T* u, const T* ec, const T* f, T* u_out, T* fc, const uint8_t* pid,
@@ -3116,7 +3230,8 @@ static int cycle_join_rects(const T* u, const T* ec, const T* f, T* u_out, T* fc
   g.nrect = nrect;
   for (int r = 0; r < nrect; ++r) {
     const int I0 = rects[4 * r], I1 = rects[4 * r + 1], c0 = rects[4 * r + 2], c1 = rects[4 * r + 3];
-    if (I0 < 1 || I1 > g.Hc - 1 || I0 >= I1 || c0 < 1 || c1 > W - 1 || c0 >= c1 || !(c0 & 1) || !(c1 & 1))
+    if (I0 < 1 || I1 > g.Hc - 1 || I0 >= I1 || c0 < 1 || c1 > W - 1 || c0 >= c1 || !(c0 & 1) ||
+        (!(c1 & 1) && c1 != W - 1))
       return FEA_EINVAL;
     g.rI0[r] = I0; g.rI1[r] = I1; g.rc0[r] = c0; g.rc1[r] = c1;
     g.rns[r] = div_up(c1 - c0, Ovl3<T>::S);

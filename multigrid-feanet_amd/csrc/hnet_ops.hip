@@ -19,6 +19,12 @@
 namespace fea {
 
 constexpr int kHMaxLayers = 3;    // HNet(nb_layers=3) (M-FEANet-mg_test.ipynb:222)
+// input rows in flight per wave (1 or 2 steps ahead).  Same-lease A/B on MI355X: profiles/r04_hjac
+#ifndef FEA_HSWEEP_PF
+#define FEA_HSWEEP_PF 2
+#endif
+constexpr int kHPrefetch = FEA_HSWEEP_PF;
+static_assert(kHPrefetch == 1 || kHPrefetch == 2, "hsweep prefetch of 1 or 2 rows");
 constexpr int kHTS = 10;          // LDS table stride (9 weights + omega/d)
 
 // ---------------------------------------------------------------------------------------------------------
@@ -285,11 +291,12 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
 #pragma unroll
   for (int k = 0; k <= V; ++k) Ra[k] = Rb[k] = T(0);
   const int y0 = rc0 - HALO, y1 = rc1 - 1 + HALO;
-  // input rows two steps ahead, in a ring of two slots indexed by the step's parity (compile-time after the
+  // input rows PF steps ahead, in a ring of PF slots indexed by the step's position (compile-time after the
   // unroll below): step y consumes u(y), pid(y), f(y-1) (RAW: u_raw(y-1); MODE 2: f and pid of its residual row
-  // y-2-NL, the iterate of its out row y-1-NL) and refills the slot with the rows of step y+2 at once
-  T ur[2][V], fr_[2][V], rw_[2][V], frr[2][V], uo[2][V];
-  int pr[2][V], po[2][V];
+  // y-2-NL, the iterate of its out row y-1-NL) and refills the slot with the rows of step y+PF at once
+  constexpr int PF = kHPrefetch;
+  T ur[PF][V], fr_[PF][V], rw_[PF][V], frr[PF][V], uo[PF][V];
+  int pr[PF][V], po[PF][V];
   // MODE 2 needs the iterate's values of an out row only where they stand in for the sweep (boundary nodes)
   auto need_uo = [&](int yy) { return !(yy >= 1 && yy <= H - 2) || !cin[0] || !cin[V - 1]; };
   auto fill = [&](int sl, int y) {
@@ -309,8 +316,8 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
       }
     }
   };
-  fill(0, y0);
-  fill(1, y0 + 1);
+#pragma unroll
+  for (int d = 0; d < PF; ++d) fill(d, y0 + d);
   // MODE 1: coarse rows floor(y/2) (Clo) and floor(y/2) + 1 (Chi) of the row entering the window; nC = the next
   CR Clo{}, Chi{};
   CRaw nC{};
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
       uout[k] = (MODE == 2 && !ZERO) ? uo[SL][k] : T(0);
       pout[k] = (MODE == 2 && MULTI) ? po[SL][k] : 0;
     }
-    if (y + 2 <= y1) fill(SL, y + 2);
+    if (y + PF <= y1) fill(SL, y + PF);
     if constexpr (MODE == 1) {
       // x(y) = u(y) + w1 P(ec) on the interior (correct_even / correct_odd of k_mg_prolong)
       const bool yin = y >= 1 && y <= H - 2;
@@ -547,11 +554,12 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
     }
   };
   int y = y0;
-  for (; y + 1 <= y1; y += 2) {
+  for (; y + PF - 1 <= y1; y += PF) {
     step(y, std::integral_constant<int, 0>{});
-    step(y + 1, std::integral_constant<int, 1>{});
+    if constexpr (PF > 1) step(y + 1, std::integral_constant<int, 1 % PF>{});
   }
-  if (y <= y1) step(y, std::integral_constant<int, 0>{});
+  if constexpr (PF > 1)
+    if (y <= y1) step(y, std::integral_constant<int, 0>{});
 }
 
 }  // namespace fea

@@ -11,6 +11,8 @@ import torch  # noqa: F401  (must precede the CDLL load)
 
 from .build import LIB
 
+_IN_TREE = LIB
+
 ABI_VERSION = 3
 
 P = ctypes.c_void_p
@@ -95,15 +97,23 @@ def lib():
         raise RuntimeError(f"feanet_amd: {LIB} is missing; run `python -m feanet_amd.build` "
                            "(there is no CPU fallback for the HIP path)")
     L = ctypes.CDLL(LIB)  # (A/B builds of tools/lab replace the module attribute LIB: tools/lab/with_lib.py)
+    lab = os.path.abspath(LIB) != os.path.abspath(_IN_TREE)  # an older lab build may lack newer entry points
+
+    def sym(name):
+        if lab and not hasattr(L, name):
+            return None
+        return getattr(L, name)
     for name, (args, res) in _EXTRA.items():
-        fn = getattr(L, name)
-        fn.argtypes = args
-        fn.restype = res
+        fn = sym(name)
+        if fn is not None:
+            fn.argtypes = args
+            fn.restype = res
     for base, args in _SIGS.items():
         for suf, S in (("f32", F32), ("f64", F64)):
-            fn = getattr(L, f"fea_{base}_{suf}")
-            fn.argtypes = [S if a == "S" else a for a in args]
-            fn.restype = I
+            fn = sym(f"fea_{base}_{suf}")
+            if fn is not None:
+                fn.argtypes = [S if a == "S" else a for a in args]
+                fn.restype = I
     if L.fea_abi_version() != ABI_VERSION:
         raise RuntimeError("feanet_amd: libfeanet_hip.so ABI version mismatch; rebuild it")
     _lib = L

@@ -380,7 +380,8 @@ class DDSolver:
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
-                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5):
+                 batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5,
+                 split_join=True):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
         self.graph_min = graph_min
@@ -413,6 +414,9 @@ class DDSolver:
         assert self.joinable() == _joined(nu1, nu2, fuse)
         self.use_graph = graph
         self._capture_ok = True
+        # captured cycles: the finest join split into border rectangles (run with the halo exchange on a side
+        # stream) and the interior (split_join; DDSolver.join_rects)
+        self.split_join = split_join
         self._segs = {}
         self._graphs = {}
         self._state = "a"
@@ -650,8 +654,10 @@ class DDSolver:
             return _rows(Lc.f, Lc.B, Lc.bs, Lc.ld, 1, 1 + self.P * c)
         if getattr(self, "_gstage", None) is None:
             cc = self.part.cols_per_rank(self.Ld)
-            self._gstage = torch.empty((self.P, self.B, c, cc), dtype=self.dtype, device=self.device)
-            self._gsend = torch.empty((self.B, c, cc), dtype=self.dtype, device=self.device)
+            # zero-filled once: a communicator that moves nothing (the projection's PackComm) then leaves a
+            # deterministic coarse right-hand side instead of whatever the allocator handed back
+            self._gstage = torch.zeros((self.P, self.B, c, cc), dtype=self.dtype, device=self.device)
+            self._gsend = torch.zeros((self.B, c, cc), dtype=self.dtype, device=self.device)
         return self._gstage
 
     def gather_place_views(self, blocks):
@@ -782,12 +788,17 @@ class DDSolver:
         pending = None  # level-0 halo exchange in flight (overlaps the coarse levels' kernels)
         for key in keys:
             segs, _ = self.chunk(key)
+            skip = -1
             for i, (kind, st, lvl0) in enumerate(segs):
+                if i == skip:
+                    continue
                 if kind == "k":
                     if lvl0 and pending is not None:
                         self.comm.exchange_finish(pending)
                         pending = None
-                    if captured:
+                    if captured and self.split_join and self._split_join(segs, i):
+                        skip = i + 1  # the exchange ran beside the interior join
+                    elif captured:
                         _launch_list(segs[i][1], self.dtype, torch.cuda.current_stream(self.device))
                     else:
                         self.run_kernels(key, i)
@@ -812,11 +823,81 @@ class DDSolver:
         if pending is not None:
             self.comm.exchange_finish(pending)
 
+    def join_rects(self):
+        """(border rectangles, interior rectangle) of the finest level's cycle join, as fea_mg_cycle_join_rects takes
+        them ({I0, I1, c0, c1}: coarse rows, odd fine-column bounds): the border holds every node the cycle's halo
+        exchange sends (owned nodes within D0 fine / D1 coarse lines of an edge with a neighbour) or receives (the
+        ghost lines), so the interior join can run while the messages are in flight."""
+        if getattr(self, "_rects", None) is not None:
+            return self._rects
+        D0, D1 = self.depths
+        p0, q0, p1, q1 = self.parts[0], self.cparts[0], self.parts[1], self.cparts[1]
+        Hc, W = self.local.levels[1].H, self.local.levels[0].W
+        up, down = self.ri > 0, self.ri < self.Pr - 1
+        left, right = self.ci > 0, self.ci < self.Pc - 1
+        odd_up = lambda x: x if x & 1 else x + 1
+        odd_down = lambda x: x if x & 1 else x - 1
+        Ia = max(p1.lo + D1, (p0.lo + D0 + 2) // 2) if up else 1
+        Ib = min(p1.hi - D1, (p0.hi - D0 + 1) // 2) if down else Hc - 1
+        ca = max(2 * (q1.lo + D1) - 1, odd_up(q0.lo + D0)) if left else 1
+        cb = min(2 * (q1.hi - D1) - 1, odd_down(q0.hi - D0)) if right else W - 1
+        if not (1 <= Ia < Ib <= Hc - 1 and 1 <= ca < cb <= W - 1):
+            self._rects = ([], None)
+            return self._rects
+        border = [r for r in ((1, Ia, 1, W - 1), (Ib, Hc - 1, 1, W - 1), (Ia, Ib, 1, ca), (Ia, Ib, cb, W - 1))
+                  if r[0] < r[1] and r[2] < r[3]]
+        self._rects = (border, (Ia, Ib, ca, cb))
+        return self._rects
+
+    def _split_join(self, segs, i):
+        """Captured cycles: a kernel segment that ends in the cycle join (+ the halo pack) followed by its halo
+        exchange runs as [the segment's other kernels] -> the border rectangles' join, the pack, the exchange and
+        the unpack on a side stream BESIDE the interior rectangle's join on the compute stream -> rejoin.  Returns
+        False (nothing issued) where the pattern or the rectangles do not apply."""
+        launches = segs[i][1]
+        if i + 1 >= len(segs) or segs[i + 1][0] != "c" or segs[i + 1][1][0] != "exchanges" or self.P == 1:
+            return False
+        nj = [k for k, (name, _) in enumerate(launches) if name == "mg_cycle_join"]
+        if len(nj) != 1 or any(name not in ("fn",) for name, _ in launches[nj[0] + 1:]):
+            return False
+        border, inner = self.join_rects()
+        if inner is None or not border:
+            return False
+        j = nj[0]
+        jargs = launches[j][1][:23]  # mg_cycle_join's arguments up to bsc (no norm)
+        rects = self.__dict__.setdefault("_rect_arrays", {})
+        arrs = []
+        for key, rs in (("border", border), ("inner", [inner])):
+            if key not in rects:
+                import ctypes
+                rects[key] = (ctypes.c_int * (4 * len(rs)))(*[x for r in rs for x in r])
+            arrs.append((len(rs), ctypes_addr(rects[key])))
+        main = torch.cuda.current_stream(self.device)
+        side = self.__dict__.get("_side")
+        if side is None:
+            side = self._side = torch.cuda.Stream(self.device)
+        _launch_list(launches[:j], self.dtype, main)
+        side.wait_stream(main)
+        st = segs[i + 1][1]
+        with torch.cuda.stream(side):
+            _launch_list([("mg_cycle_join_rects", jargs + arrs[0])] + launches[j + 1:], self.dtype, side)
+            now, later = _split_exchanges(st[1], self.overlap_l0)
+            items = list(now) + list(later)
+            self.comm.exchange_many(self, items, packed=len(st) > 2 and st[2])
+        _launch_list([("mg_cycle_join_rects", jargs + arrs[1])], self.dtype, main)
+        main.wait_stream(side)
+        return True
+
     def residual_norm(self):
         n2 = self.residual_norm_sq_local()
         if self.comm is not None:
             n2 = self.comm.allreduce_sum(n2)
         return torch.sqrt(n2)
+
+
+def ctypes_addr(arr):
+    import ctypes
+    return ctypes.addressof(arr)
 
 
 def _boundary_mask(H, W, like):

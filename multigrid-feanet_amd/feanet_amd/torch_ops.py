@@ -202,7 +202,12 @@ def mg_step(u: Tensor, f: Tensor, solver: int, cycles: int = 1) -> Tensor:
     the fine iterate u with right-hand side f; returns the new iterate [B, 1, H, W].  The solver's level
     buffers, HIP graphs and schedule stay resident between calls: this op is the whole-cycle form of
     MultiGrid.Step(v, f) (one pass per fused level kernel) that a notebook loop can call as
-    `u = torch.ops.feanet.mg_step(u, f, solver.handle)`."""
+    `u = torch.ops.feanet.mg_step(u, f, solver.handle)`.
+
+    Contract: only the returned tensor is defined.  The op is registered functional (mutates_args=()), so
+    under torch.compile an op whose result is unused may be dropped, and ops may be reordered against direct
+    calls of the solver's methods: what solver.solution() / residual_norm() return after it is not part of
+    the op's meaning (read the returned tensor instead)."""
     from .solver import solver_by_handle
     return solver_by_handle(solver)._step(u, f, cycles)
 

@@ -210,18 +210,22 @@ class _FakeDist:
         t.copy_(sum(self._gather(t)))
 
 
+@pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("overlap_l0", [False, True])
 @pytest.mark.parametrize("m,n,P,Ld,grid", [(512, 256, 2, 2, (2, 1)), (512, 512, 4, 2, (2, 2)), (512, 1024, 8, 2, (4, 2))])
-def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0):
+def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph):
     """TorchComm's RCCL branch (device views sent directly when contiguous; otherwise the one-phase packed
     batch with its pack inside the kernel segment, one message per neighbour including the diagonal ones;
     with overlap_l0 the deferred level-0 exchange; all_gather_into_tensor into the coarse f, all_reduce of
     the norm) with the ranks as threads over an in-process fake of the nccl backend: bitwise the
-    single-GPU V-cycle.  This is the path the multi-GPU bench takes; one GPU cannot host two RCCL ranks."""
+    single-GPU V-cycle.  This is the path the multi-GPU bench takes; one GPU cannot host two RCCL ranks.
+    graph=True: every chunk shape runs three times (eager, captured, replayed), so the halo pack ('fn' step) and
+    the gather staging / placement copies are checked inside replayed HIP graph segments too."""
     import threading
     from feanet_amd.dd import DDSolver, TorchComm
     f, u0, bc = _global_problem(m, n, 1, seed=3)
-    _, ref = _single(m, n, 1, f, u0, bc, 3)
+    calls = (1, 1, 1, 2, 2, 2) if graph else (1, 2)
+    _, ref = _single(m, n, 1, f, u0, bc, sum(calls))
     torch.cuda.synchronize()
     fake = _FakeDist(P)
     out, errs = {}, []
@@ -231,11 +235,12 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0):
             fake.tls.rank = r
             comm = TorchComm(dist=fake)
             assert comm.gpu and comm.rank == r
-            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=False, overlap_l0=overlap_l0)
+            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=graph, overlap_l0=overlap_l0,
+                         **({"graph_min": 1} if graph else {}))
             s.set_rhs(f)
             s.load(u0, bc)
-            s.vcycle(1)
-            s.vcycle(2)  # joined cycles: the deferred level-0 halo finish
+            for k in calls:  # vcycle(2): joined cycles, the deferred level-0 halo finish
+                s.vcycle(k)
             out[r] = (s.owned_block(), s.residual_norm())
         except Exception as e:  # noqa: BLE001
             errs.append((r, e))
@@ -259,3 +264,38 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0):
     if grid[1] > 1:
         assert any(ya != yb and xa != xb for (ya, xa), (yb, xb) in pairs)
     assert not fake.mail, "unmatched messages"
+
+
+@pytest.mark.parametrize("P,grid,rank,n", [(8, (4, 2), 3, 1024), (4, (2, 2), 0, 512), (2, (2, 1), 1, 512)])
+def test_dd_captured_cycles_match_segments(P, grid, rank, n):
+    """DDSolver with a capturable communicator runs whole blocks of cycles as HIP graphs — kernels AND the halo
+    exchange, the finest join split into border rectangles (beside which the exchange runs on a side stream) and
+    the interior (DDSolver.join_rects) — and must issue exactly the segment-wise path's work: one rank's buffers
+    are bitwise equal after the eager, captured and replayed blocks.  The communicator moves nothing (the
+    projection's PackComm: pack, unpack of a zero staging buffer, no all-gather), so both runs are deterministic."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from tools.dd_projection import PackComm
+    from feanet_amd.dd import DDSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(P + rank)
+    f = torch.randn(1, 1, n + 1, n + 1, device="cuda", dtype=torch.float64, generator=g)
+    outs = []
+    for capture, split in ((False, False), (True, False), (True, True)):
+        comm = PackComm()
+        comm.capturable = capture
+        s = DDSolver(n, n, rank, P, comm=comm, agglomerate=2, grid=grid, split_join=split)
+        if split:
+            border, inner = s.join_rects()
+            assert inner is not None and border
+        s.set_rhs(f)
+        s.load()
+        for k in (1, 3, 3, 3, 2):  # eager, then captured, then replayed blocks of joined cycles
+            s.vcycle(k)
+        torch.cuda.synchronize()
+        L0 = s.local.levels[0]
+        outs.append((L0.view(L0.buf(s._state)).clone(), s.local.levels[1].view(s.local.levels[1].f).clone()))
+        if capture:
+            assert any(v is not None for v in s._graphs.values())
+    for a, b in zip(outs[1:], outs[:1] * 2):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
