@@ -598,8 +598,51 @@ static void hs_dispatch(bool multi, bool zero, bool raw, int nl, dim3 grid, hipS
   }
 }
 
-// rows per task: the largest of 64 / 32 / 16 / 8 that still gives >= 2048 waves (each task recomputes nl + 1
-// (MODE 2: nl + 2) rows above and below its own)
+static int hs_num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+#ifndef FEA_HSWEEP_BALANCED
+#define FEA_HSWEEP_BALANCED 1
+#endif
+
+// Row tasks: `unit` rows each (MODE 2 counts coarse rows, 2 fine rows per unit), a task streams k*unit + ovh
+// rows (the stage chain's halo rows above and below its own).  Balanced (the cycle join's rule, framed_ops.hip
+// balanced_rb): the slowest CU runs ceil(workgroups / CUs) tasks back to back, so the cost of a task height is
+// that count times the rows a task streams; among the heights that keep >= 2048 waves in flight the cheapest
+// wins (4097^2 fp64 sweep+restriction: 504 workgroups of 74 rows, 2 per CU, instead of 576 of 64: a quarter of
+// the CUs ran a third task).  Levels too small for 2048 waves at any height take the cheapest height outright:
+// there every CU holds at most one or two tasks and the task's chain of rows is the time.  Results are bitwise
+// independent of the task height.
+static int hs_units_per_task(int B, int nstrips, int rows_u, int k, int ovh) {
+#if FEA_HSWEEP_BALANCED
+  const long long ncu = hs_num_cus();
+  long long best_ok = -1, best_any = -1;
+  int u_ok = 0, u_any = 1;
+  for (int u = 1; u <= rows_u && k * u <= 256; ++u) {
+    const long long ntr = (rows_u + u - 1) / u, waves = (long long)B * nstrips * ntr;
+    const long long wgs = (long long)B * ((ntr * nstrips + 3) / 4);
+    const long long cost = ((wgs + ncu - 1) / ncu) * (k * u + ovh);
+    if (waves >= 2048 && (best_ok < 0 || cost < best_ok)) best_ok = cost, u_ok = u;
+    if (best_any < 0 || cost < best_any) best_any = cost, u_any = u;
+  }
+  return best_ok >= 0 ? u_ok : u_any;
+#else
+  // the largest of 64 / 32 / 16 / 8 rows that still gives >= 2048 waves
+  for (int rb = 64; rb > 8; rb /= 2)
+    if ((long long)B * nstrips * ((rows_u * k + rb - 1) / rb) >= 2048) return rb / k;
+  return 8 / k;
+#endif
+}
+
 template <typename T, int MODE>
 static int hsweep_launch(HSArgs<T> g, int nl, int B, hipStream_t s) {
   constexpr int V = HVec<T>::V;
@@ -608,14 +651,11 @@ static int hsweep_launch(HSArgs<T> g, int nl, int B, hipStream_t s) {
   // (lanes past the grid's last column re-read the last valid line: loads stay within columns < W + V)
   g.nstrips = (g.W - 2 + S - 1) / S;
   const int rows = MODE == 2 ? g.Hc - 2 : g.H - 2;  // MODE 2 tasks count coarse rows (rb / 2 each)
-  const int per = MODE == 2 ? 2 : 1;
-  g.rb = 8;
-  for (int rb = 64; rb > 8; rb /= 2)
-    if ((long long)B * g.nstrips * ((rows * per + rb - 1) / rb) >= 2048) {
-      g.rb = rb;
-      break;
-    }
-  g.ntr = MODE == 2 ? (rows + g.rb / 2 - 1) / (g.rb / 2) : (rows + g.rb - 1) / g.rb;
+  const int k = MODE == 2 ? 2 : 1;
+  const int ovh = 2 * (nl + 1) + (MODE == 2 ? 2 : 0);
+  const int u = hs_units_per_task(B, g.nstrips, rows, k, ovh);
+  g.rb = k * u;
+  g.ntr = (rows + u - 1) / u;
   const dim3 grid((unsigned)(B * ((g.ntr * g.nstrips + 3) / 4)));
   hs_dispatch<T, MODE>(g.ntab > 1, !g.u, g.u_raw != nullptr, nl, grid, s, g);
   FEA_LAUNCH_CHECK();

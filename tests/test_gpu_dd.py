@@ -143,6 +143,7 @@ class _FakeDist:
         self.tls = threading.local()
         self.isend, self.irecv = "isend", "irecv"
         self.posted = []  # (src, dst, numel) in posting order, for the test's own checks
+        self.gpu_lock = threading.RLock()  # the fake's device copies never run beside another rank's capture
 
         class P2POp:
             def __init__(op, kind, tensor, peer, group=None):
@@ -165,7 +166,8 @@ class _FakeDist:
             for op in ops:
                 if op.kind == "isend":
                     k = (me, op.peer)
-                    self.mail[k + (self.nsend[k],)] = op.tensor.clone()
+                    with self.gpu_lock:
+                        self.mail[k + (self.nsend[k],)] = op.tensor.clone()
                     self.posted.append((me, op.peer, op.tensor.numel()))
                     self.nsend[k] += 1
             self.cv.notify_all()
@@ -182,7 +184,8 @@ class _FakeDist:
                     fake.cv.wait_for(lambda: w.key in fake.mail, timeout=60)
                     src = fake.mail.pop(w.key)
                 assert src.shape == w.t.shape or src.numel() == w.t.numel(), (src.shape, w.t.shape)
-                w.t.copy_(src.reshape(w.t.shape))
+                with fake.gpu_lock:
+                    w.t.copy_(src.reshape(w.t.shape))
                 w.key = None
         for op in ops:
             if op.kind == "irecv":
@@ -193,27 +196,34 @@ class _FakeDist:
 
     def _gather(self, t):
         me = self.tls.rank
-        self.slots[me] = t.clone()
+        with self.gpu_lock:
+            self.slots[me] = t.clone()
         self.bar.wait()
         parts = list(self.slots)
         self.bar.wait()
         return parts
 
     def all_gather_into_tensor(self, out, inp, group=None):
-        out.copy_(torch.cat([p.reshape(-1) for p in self._gather(inp)]))
+        parts = self._gather(inp)
+        with self.gpu_lock:
+            out.copy_(torch.cat([p.reshape(-1) for p in parts]))
 
     def all_gather(self, parts, src, group=None):
-        for d, s in zip(parts, self._gather(src)):
-            d.copy_(s)
+        got = self._gather(src)
+        with self.gpu_lock:
+            for d, s in zip(parts, got):
+                d.copy_(s)
 
     def all_reduce(self, t, group=None, op=None):
-        t.copy_(sum(self._gather(t)))
+        parts = self._gather(t)
+        with self.gpu_lock:
+            t.copy_(sum(parts))
 
 
 @pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("overlap_l0", [False, True])
 @pytest.mark.parametrize("m,n,P,Ld,grid", [(512, 256, 2, 2, (2, 1)), (512, 512, 4, 2, (2, 2)), (512, 1024, 8, 2, (4, 2))])
-def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph):
+def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph, monkeypatch):
     """TorchComm's RCCL branch (device views sent directly when contiguous; otherwise the one-phase packed
     batch with its pack inside the kernel segment, one message per neighbour including the diagonal ones;
     with overlap_l0 the deferred level-0 exchange; all_gather_into_tensor into the coarse f, all_reduce of
@@ -229,19 +239,32 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph):
     torch.cuda.synchronize()
     fake = _FakeDist(P)
     out, errs = {}, []
+    if graph:
+        # one GPU hosts every rank here: a rank's kernel segment (eager, captured or replayed) runs while no other
+        # rank captures or allocates (the fake's snapshots allocate), as with one process per GPU
+        orig = DDSolver.run_kernels
+
+        def run_kernels(self, key, i):
+            with fake.gpu_lock:
+                orig(self, key, i)
+        monkeypatch.setattr(DDSolver, "run_kernels", run_kernels)
 
     def run(r):
         try:
             fake.tls.rank = r
             comm = TorchComm(dist=fake)
             assert comm.gpu and comm.rank == r
-            s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=graph, overlap_l0=overlap_l0,
-                         **({"graph_min": 1} if graph else {}))
-            s.set_rhs(f)
-            s.load(u0, bc)
-            for k in calls:  # vcycle(2): joined cycles, the deferred level-0 halo finish
-                s.vcycle(k)
-            out[r] = (s.owned_block(), s.residual_norm())
+            # each rank on its own (non-default) stream, as each process of a real run: no rank's work goes to
+            # the legacy default stream, which would synchronise with (and break) another rank's graph capture
+            with torch.cuda.stream(torch.cuda.Stream()):
+                s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=graph, overlap_l0=overlap_l0,
+                             **({"graph_min": 1} if graph else {}))
+                s.set_rhs(f)
+                s.load(u0, bc)
+                for k in calls:  # vcycle(2): joined cycles, the deferred level-0 halo finish
+                    s.vcycle(k)
+                out[r] = (s.owned_block(), s.residual_norm())
+                torch.cuda.current_stream().synchronize()
         except Exception as e:  # noqa: BLE001
             errs.append((r, e))
             fake.bar.abort()
