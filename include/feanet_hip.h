@@ -460,6 +460,11 @@ long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int
  * its stage (row-major, rows x cols), 0 back out of it.  elem_size 4 or 8.  No reference counterpart (the
  * reference is single-process): it packs the messages of the new multi-GPU path. */
 int fea_dd_copy_blocks(const void* blocks, int nblocks, int elem_size, int to_stage, void* stream);
+/* Strided rectangle copies in one launch (the agglomeration's all-gather staging / placement and the coarse
+ * solution's scatter, feanet_amd.dd): rects is a HOST array of nrects records {int64 dst, int64 src (device
+ * addresses of the first elements), int64 dst_ld, int64 src_ld (row pitches, elements), int64 rows, int64 cols},
+ * copied into the kernel arguments (32 per launch).  elem_size 4 or 8.  No reference counterpart. */
+int fea_dd_copy_rects(const void* rects, int nrects, int elem_size, void* stream);
 
 /* On-device mesh set-up: the MeshCenterInterface node pattern map — replaces
  * FEANet/mesh.py place_circle / place_rect (:62-76), identify_patterns (:78-93) and

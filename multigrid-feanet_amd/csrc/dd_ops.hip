@@ -36,9 +36,66 @@ __global__ __launch_bounds__(256) void k_dd_copy_blocks(const DDTable tab, int t
   }
 }
 
+// Strided rectangle copies (the agglomeration's all-gather staging, the placement of the gathered blocks into the
+// coarse field and the scatter of the coarse solution back): both sides strided, any number of rectangles in
+// one launch.  Latency-bound like the halo pack, so the grid spreads a rectangle over up to 256 workgroups
+// (one element per thread) instead of looping.
+struct DDRect {     // (mirrors feanet_amd/dd.py _rect_records: 6 int64 words)
+  long long dst, src;        // device addresses of the rectangles' first elements
+  long long dst_ld, src_ld;  // row pitches, elements
+  long long rows, cols;
+};
+
+constexpr int kDDRects = 32;  // rectangles per launch (1.5 KB of kernel arguments)
+
+struct DDRectTable {
+  DDRect r[kDDRects];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_dd_copy_rects(const DDRectTable tab) {
+  const DDRect q = tab.r[blockIdx.y];
+  T* __restrict__ dst = reinterpret_cast<T*>(q.dst);
+  const T* __restrict__ src = reinterpret_cast<const T*>(q.src);
+  const int cols = (int)q.cols;
+  const int n = (int)(q.rows * q.cols);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int r = i / cols, c = i - r * cols;
+    dst[r * q.dst_ld + c] = src[r * q.src_ld + c];
+  }
+}
+
 }  // namespace fea
 
 using namespace fea;
+
+extern "C" int fea_dd_copy_rects(const void* rects, int nrects, int elem_size, void* stream) {
+  if (!rects || nrects <= 0 || (elem_size != 4 && elem_size != 8)) return FEA_EINVAL;
+  const DDRect* all = static_cast<const DDRect*>(rects);
+  hipStream_t s = (hipStream_t)stream;
+  for (int r0 = 0; r0 < nrects; r0 += kDDRects) {
+    DDRectTable tab{};
+    const int nr = std::min(kDDRects, nrects - r0);
+    long long mx = 1;
+    for (int i = 0; i < nr; ++i) {
+      const DDRect& q = all[r0 + i];
+      const long long n = q.rows * q.cols;
+      if (q.rows < 0 || q.cols <= 0 || n >= (1ll << 31) || !q.dst || !q.src || q.dst_ld < q.cols ||
+          q.src_ld < q.cols)
+        return FEA_EINVAL;
+      tab.r[i] = q;
+      mx = std::max(mx, n);
+    }
+    const dim3 grid((unsigned)std::min<long long>((mx + 255) / 256, 256), (unsigned)nr);
+    if (elem_size == 8)
+      k_dd_copy_rects<double><<<grid, 256, 0, s>>>(tab);
+    else
+      k_dd_copy_rects<float><<<grid, 256, 0, s>>>(tab);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
 
 extern "C" int fea_dd_copy_blocks(const void* blocks, int nblocks, int elem_size, int to_stage, void* stream) {
   if (!blocks || nblocks <= 0 || (elem_size != 4 && elem_size != 8)) return FEA_EINVAL;
@@ -55,7 +112,7 @@ extern "C" int fea_dd_copy_blocks(const void* blocks, int nblocks, int elem_size
         return FEA_EINVAL;
       mx = std::max(mx, n);
     }
-    const dim3 grid((unsigned)std::min<long long>((mx + 255) / 256, 64), (unsigned)nb);
+    const dim3 grid((unsigned)std::min<long long>((mx + 255) / 256, 256), (unsigned)nb);
     if (elem_size == 8)
       k_dd_copy_blocks<double><<<grid, 256, 0, s>>>(tab, to_stage);
     else

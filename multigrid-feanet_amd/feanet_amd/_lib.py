@@ -72,6 +72,7 @@ _EXTRA = {
     "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
     "fea_interface_pattern_map": ([P, LL, I, I, F64, P], I),
     "fea_dd_copy_blocks": ([P, I, I, I, P], I),
+    "fea_dd_copy_rects": ([P, I, I, P], I),
     "fea_stencil_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),
     "fea_stencil_weight_grad_ws_bytes_f64": ([I, I, I, I], ctypes.c_size_t),
     "fea_transfer_weight_grad_ws_bytes_f32": ([I, I, I, I], ctypes.c_size_t),

@@ -334,16 +334,71 @@ def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None):
 
 
 def _launch_list(launches, dtype, stream):
-    """C-ABI calls, ("copy", (dst, src)) device copies and ("fn", f) device steps f(stream), in order, on
-    `stream`."""
+    """C-ABI calls, ("copy", (dst, src)) device copies, ("rects", (records, elem_size)) strided rectangle copies
+    (fea_dd_copy_rects) and ("fn", f) device steps f(stream), in order, on `stream`."""
     for name, args in launches:
         if name == "copy":
             with torch.cuda.stream(stream):
                 args[0].copy_(args[1])
+        elif name == "rects":
+            _lib.call_raw("dd_copy_rects", args[0].ctypes.data, len(args[0]), args[1], stream.cuda_stream)
         elif name == "fn":  # a communicator's device step (halo pack), launched on `stream`
             args(stream)
         else:
             _lib.call(name, dtype, *args, stream.cuda_stream)
+
+
+_DD_RECT_WORDS = 6  # fea_dd_copy_rects record: int64 dst, src, dst_ld, src_ld, rows, cols
+
+
+def _rect_records(dst, src):
+    """A device copy dst <- src between two equal-shape strided views as fea_dd_copy_rects records (host int64
+    [n, 6]): the columns are the dimension of unit stride in both, the rows the largest other dimension, one
+    rectangle per index of the remaining ones.  None when the views do not decompose so (no unit-stride
+    dimension in common, a row pitch below the row length, different dtypes or devices)."""
+    import itertools
+    import numpy as np
+    if dst.shape != src.shape or dst.dtype != src.dtype or dst.device != src.device or dst.numel() == 0:
+        return None
+    dims = [k for k in range(dst.dim()) if dst.shape[k] > 1]
+    cols = [k for k in dims if dst.stride(k) == 1 and src.stride(k) == 1]
+    if not cols:
+        if dims:
+            return None
+        cols = [dst.dim() - 1] if dst.dim() else []
+    if not cols:
+        return None
+    k = cols[0]
+    rest = [d for d in dims if d != k]
+    r = max(rest, key=lambda d: dst.shape[d]) if rest else None
+    nrows = dst.shape[r] if r is not None else 1
+    ncols = dst.shape[k]
+    dld = dst.stride(r) if r is not None else ncols
+    sld = src.stride(r) if r is not None else ncols
+    if dld < ncols or sld < ncols:
+        return None
+    esz = dst.element_size()
+    outer = [d for d in rest if d != r]
+    recs = []
+    for idx in itertools.product(*[range(dst.shape[d]) for d in outer]):
+        do = sum(i * dst.stride(d) for i, d in zip(idx, outer))
+        so = sum(i * src.stride(d) for i, d in zip(idx, outer))
+        recs.append((dst.data_ptr() + do * esz, src.data_ptr() + so * esz, dld, sld, nrows, ncols))
+    return np.array(recs, dtype=np.int64).reshape(-1, _DD_RECT_WORDS)
+
+
+def _as_rect_copies(launches):
+    """("copy", (dst, src)) launches -> ("rects", (records, elem_size)) where the views decompose (one
+    fea_dd_copy_rects launch instead of a generic strided-copy kernel)."""
+    out = []
+    for name, args in launches:
+        if name == "copy":
+            recs = _rect_records(*args)
+            if recs is not None:
+                out.append(("rects", (recs, args[0].element_size())))
+                continue
+        out.append((name, args))
+    return out
 
 
 def _split_exchanges(items, overlap_l0=False):
@@ -376,12 +431,16 @@ class DDSolver:
     the coarse solve) instead of with the coarse-level halo in one batch — one more message group and one
     more unpack launch per cycle; graph_min: kernel segments of fewer launches run eagerly instead of as HIP
     graphs (on this chip a graph launch between two communication steps costs ~8 us of GPU time, a short
-    eager segment less); other args as MultigridSolver (Poisson).
+    eager segment less); split_join (captured cycles only): the finest join as border rectangles + the halo
+    exchange on a side stream beside the interior rectangle — off by default: on one GPU (8-rank projection,
+    8193^2, 4x2) the split costs 142 instead of 117 us per cycle (thin border rectangles are mostly pipeline
+    fill, the interior shares the CUs with them), more than an exchange of this size takes; overlap_l0
+    overlaps the level-0 halo with the coarse levels instead; other args as MultigridSolver (Poisson).
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
                  batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5,
-                 split_join=True):
+                 split_join=False):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
         self.graph_min = graph_min
@@ -506,7 +565,11 @@ class DDSolver:
             # computations on the same local nodes, so the ghost validity of every step is unchanged)
             ok = lambda l: l >= 1 and l + 2 <= self.Ld
             steps = pair_prolongations(pair_restrictions(steps, ok), ok)
-        for st in steps:
+        direct = None  # ("scatter", dst) folded into the next launch: it reads the coarse solution in place
+        for si, st in enumerate(steps):
+            if st[0] == "scatter" and self._scatter_direct(st, steps[si + 1] if si + 1 < len(steps) else None):
+                direct = st
+                continue
             if st[0] == "exchange":  # consecutive exchanges go out as one batch of P2P ops
                 if self.P == 1:
                     continue  # no neighbours
@@ -537,6 +600,8 @@ class DDSolver:
                 launches = [self.local._join_call(st[1], self.local._ptr(1, st[2]))]
             else:
                 launches = [self.local.bind_step(st)]
+                if direct is not None:
+                    launches, direct = [self._read_coarse_in_place(launches[0])], None
             if place is not None:
                 launches, place = [place] + launches, None
             if segs and segs[-1][0] == "k":
@@ -553,7 +618,34 @@ class DDSolver:
                     if f is not None:
                         segs[i - 1][1].append(("fn", f))
                     segs[i] = ("c", ("exchanges", st[1], True), False)
-        return segs
+        return [(kind, _as_rect_copies(st), lvl0) if kind == "k" else (kind, st, lvl0) for kind, st, lvl0 in segs]
+
+    def _scatter_direct(self, st, nxt):
+        """Can the scatter step `st` (coarse solution -> level Ld's buffer st[1]) be dropped, the next step reading
+        the coarse solver's buffer in place?  Only for a level-pair prolongation ("prolong_sweep2" at Ld - 2, whose
+        kernel reads the level-Ld values element by element: any row pitch and alignment) on pattern-free levels.
+        Local level Ld's frame is a window of the coarse field (local row / column 0 = global gr0 / gc0), so
+        every node the step's valid outputs use holds the same value; only the window's outer frame line (rows
+        / columns -1 and H) then shows the global neighbours instead of the local frame's padding, which reaches
+        ghost nodes the exchange depths already treat as invalid."""
+        if nxt is None or nxt[0] != "prolong_sweep2" or nxt[1] + 2 != self.Ld or nxt[2] != st[1]:
+            return False
+        return self.local.levels[self.Ld].pid is None and self.coarse.levels[0].pid is None
+
+    def _read_coarse_in_place(self, launch):
+        """mg_prolong2's launch with its level-(l+2) correction (argument 1; row pitch and sample stride: the last
+        two arguments) taken from the coarse solver's solution window of this rank instead of level Ld."""
+        name, args = launch
+        assert name == "mg_prolong2", name
+        Lc = self.coarse.levels[0]
+        pl = self.parts[self.Ld]
+        gc0 = self.cparts[self.Ld].gr0 if self.Pc > 1 else 0
+        buf = Lc.buf(self.coarse_end)
+        win = buf.data_ptr() + (pl.gr0 * Lc.ld + gc0) * buf.element_size()
+        args = list(args)
+        args[1] = win
+        args[-2], args[-1] = Lc.ld, Lc.bs
+        return (name, tuple(args))
 
     def joinable(self):
         return self.local._joinable()
