@@ -15,6 +15,7 @@
 #include "fea_common.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace fea {
 
@@ -26,6 +27,41 @@ constexpr int kHMaxLayers = 3;    // HNet(nb_layers=3) (M-FEANet-mg_test.ipynb:2
 constexpr int kHPrefetch = FEA_HSWEEP_PF;
 static_assert(kHPrefetch == 1 || kHPrefetch == 2, "hsweep prefetch of 1 or 2 rows");
 constexpr int kHTS = 10;          // LDS table stride (9 weights + omega/d)
+// FEA_HS_WRELOAD: the stencil / HNet / transfer weights (up to 46 doubles: more than the SGPR file holds beside
+// the kernel's addresses) are re-read with scalar loads at every row step instead of being hoisted once — hoisted,
+// the compiler parks them in VGPR lanes and pays a v_readlane per 32-bit half at every use (~95 VALU per step
+// of the fp64 sweep+restriction, as many as its FMAs).
+#ifndef FEA_HS_WRELOAD
+#define FEA_HS_WRELOAD 1
+#endif
+
+// steps per loop body: 6 (the 3-row windows' period x the 2-slot ring: the window rotations become register
+// renamings) for the sweep+restriction of a stored iterate, 2 elsewhere (the longer body costs those kernels their
+// third wave per SIMD: 4097^2 fp64 sweep+restriction 133.4 -> 116.8 us at 6, prolongation+sweep 103.5 -> 114.2 us;
+// same-lease A/B, profiles/r04_hjac).  FEA_HS_UNROLL overrides both (lab builds).
+template <int MODE, bool ZERO>
+constexpr int hs_unroll_steps() {
+#ifdef FEA_HS_UNROLL
+  return FEA_HS_UNROLL;
+#else
+  return (MODE == 2 && !ZERO) ? 6 : 2;
+#endif
+}
+
+template <int N, typename Fn, int... I>
+__device__ __forceinline__ void hs_unroll_(Fn&& fn, std::integer_sequence<int, I...>) {
+  (fn(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void hs_unroll(Fn&& fn) {
+  hs_unroll_<N>(fn, std::make_integer_sequence<int, N>{});
+}
+
+// a read-only load through the constant address space: scalar (s_load) for a uniform address
+template <typename T>
+__device__ __forceinline__ T cload(const T* p, int i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
 
 // ---------------------------------------------------------------------------------------------------------
 // Streaming form (the one the API launches): a wave owns a strip of S columns and marches down its rows with
@@ -120,6 +156,7 @@ struct HSArgs {
   int H, W, ld;
   long long bs;
   int nstrips, ntr, rb;
+  int zmask;  // 0 (FEA_HS_WRELOAD: an offset the compiler cannot fold)
   // MODE 1 (prolongation + correction first): the sweep's iterate is x = u + w1 P(ec)
   const T* ec;
   const uint8_t* pidc;
@@ -290,7 +327,9 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
   HWin<int, V> PRa{}, PRb{};
 #pragma unroll
   for (int k = 0; k <= V; ++k) Ra[k] = Rb[k] = T(0);
-  const int y0 = rc0 - HALO, y1 = rc1 - 1 + HALO;
+  // the first step's row is even (one more fill step on odd starts: nothing it computes is stored), so every
+  // unrolled step knows its row parity at compile time
+  const int y0 = (rc0 - HALO) & ~1, y1 = rc1 - 1 + HALO;
   // input rows PF steps ahead, in a ring of PF slots indexed by the step's position (compile-time after the
   // unroll below): step y consumes u(y), pid(y), f(y-1) (RAW: u_raw(y-1); MODE 2: f and pid of its residual row
   // y-2-NL, the iterate of its out row y-1-NL) and refills the slot with the rows of step y+PF at once
@@ -327,8 +366,26 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
     Chi = crow_fin(crow_ld(a0 + 1));
     nC = crow_ld(a0 + 2);
   }
-  auto step = [&](int y, auto slot_c) {
-    constexpr int SL = decltype(slot_c)::value;
+  auto step = [&](int y, auto pos_c) __attribute__((always_inline)) {
+    constexpr int SL = decltype(pos_c)::value % PF;
+    constexpr bool ODD = decltype(pos_c)::value & 1;  // y odd (y0 is even)
+#if FEA_HS_WRELOAD
+    {
+      const int z = y & g.zmask;  // 0 at run time, unknown to the compiler: the loads stay in the step
+      if constexpr (!MULTI) {
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+          ks[d] = cload(g.ktab, z + d);
+          if constexpr (MODE != 0) t2[d] = cload(MODE == 1 ? g.ptab : g.rtab, z + d);
+        }
+        om = cload(g.omd, z);
+      }
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int d = 0; d < 9; ++d) hk[l][d] = cload(g.hw, z + l * 9 + d);
+    }
+#endif
     // this step's rows (their loads were issued two steps ago), then the slot's refill for step y+2
     T uy[V], fy1[V], raw[V], fres[V], uout[V];
     int py[V], pout[V];
@@ -342,21 +399,22 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
       uout[k] = (MODE == 2 && !ZERO) ? uo[SL][k] : T(0);
       pout[k] = (MODE == 2 && MULTI) ? po[SL][k] : 0;
     }
-    if (y + PF <= y1) fill(SL, y + PF);
+    fill(SL, y + PF);  // (rows past the task's last are clamped into the frame: loaded, never used)
     if constexpr (MODE == 1) {
       // x(y) = u(y) + w1 P(ec) on the interior (correct_even / correct_odd of k_mg_prolong)
       const bool yin = y >= 1 && y <= H - 2;
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        if (!(yin && cin[k])) continue;
-        if (!(y & 1)) {
-          uy[k] += g.w1 * cterm(Clo, k, 1);
+      for (int k = 0; k < V; ++k) {  // (branch-free: a select, not a divergent branch per column)
+        T xk;
+        if constexpr (!ODD) {
+          xk = uy[k] + g.w1 * cterm(Clo, k, 1);
         } else {
           const T tt = cterm(Clo, k, 2) + cterm(Chi, k, 0);
-          uy[k] += g.w1 * tt;
+          xk = uy[k] + g.w1 * tt;
         }
+        uy[k] = (yin && cin[k]) ? xk : uy[k];
       }
-      if (y & 1) {  // the next row (even) starts the next coarse row pair
+      if constexpr (ODD) {  // the next row (even) starts the next coarse row pair
         Clo = Chi;
         Chi = crow_fin(nC);
         nC = crow_ld((y >> 1) + 3);
@@ -504,7 +562,7 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
           r[k] = fr[k] - acc;
         }
         r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
-        if ((yr & 1) == 0) {  // row 2I
+        if constexpr (((ODD ? 1 : 0) + NL) % 2 == 0) {  // row 2I (yr = y - 2 - NL)
 #pragma unroll
           for (int k = 0; k <= V; ++k) Rb[k] = r[k];
           PRb = Q1;
@@ -553,13 +611,14 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
       }
     }
   };
+  // the loop body holds U steps (hs_unroll_steps), the remainder one by one
+  constexpr int U = hs_unroll_steps<MODE, ZERO>();
+  static_assert(U % PF == 0 && U % 2 == 0, "hsweep unroll: even, a multiple of the prefetch ring");
   int y = y0;
-  for (; y + PF - 1 <= y1; y += PF) {
-    step(y, std::integral_constant<int, 0>{});
-    if constexpr (PF > 1) step(y + 1, std::integral_constant<int, 1 % PF>{});
-  }
-  if constexpr (PF > 1)
-    if (y <= y1) step(y, std::integral_constant<int, 0>{});
+  for (; y + U - 1 <= y1; y += U) hs_unroll<U>([&](auto i) __attribute__((always_inline)) { step(y + decltype(i)::value, i); });
+  hs_unroll<U - 1>([&](auto i) __attribute__((always_inline)) {
+    if (y + decltype(i)::value <= y1) step(y + decltype(i)::value, i);
+  });
 }
 
 }  // namespace fea
