@@ -3278,6 +3278,33 @@ FEA_JOIN_RECTS_API(f64, double)
 constexpr int kZr2MinRb = FEA_ZR2_MINRB;
 constexpr int kZr2Waves = FEA_ZR2_WAVES;
 
+// Two-level kernels (zero_restrict2, prolong2): task height by the balanced rule (balanced_rb's cost: the slowest
+// CU's workgroup count x the rows a task streams, u units of k fine rows + ovh recomputed rows), among heights
+// that keep >= 2048 waves and are at most umax units tall; the power-of-two choice `fallback` when none does.  e.g. the 2049^2 fp64 level-pair
+// prolongation: 662 workgroups of 14 rows (<= 3 per CU) instead of 576 of 16 (a quarter of the CUs ran 3 of the
+// 2.25 average).
+#ifndef FEA_BAL2
+#define FEA_BAL2 1
+#endif
+static int balanced_units(int B, int nstrips, int rows_u, int k, int ovh, int fallback, int umax = 256) {
+#if FEA_BAL2
+  const long long ncu = num_cus();
+  long long best = -1;
+  int bu = fallback;
+  for (int u = 1; u <= rows_u && u <= umax && k * u <= 256; ++u) {
+    const long long ntr = div_up(rows_u, u), waves = (long long)B * nstrips * ntr;
+    if (waves < 2048) break;
+    const long long wgs = (long long)B * div_up(ntr * nstrips, kWaves);
+    const long long cost = div_up(wgs, ncu) * (k * u + ovh);
+    if (best < 0 || cost < best) best = cost, bu = u;
+  }
+  return bu;
+#else
+  (void)B; (void)nstrips; (void)rows_u; (void)k; (void)ovh; (void)umax;
+  return fallback;
+#endif
+}
+
 template <typename T>
 static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const uint8_t* pidc, const T* ktab,
                           const T* omd, int ntab, const T* rtab, int nrtab, T w0, int B, int H, int W, int ld,
@@ -3298,6 +3325,7 @@ static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const u
   g.nstrips = div_up(W - 2, Ovl2<T>::S);
   g.rb = 2 * kRB;
   while (g.rb > kZr2MinRb && (long long)B * g.nstrips * div_up(g.Hc2 - 2, g.rb / 4) < kZr2Waves) g.rb /= 2;
+  g.rb = 4 * balanced_units(B, g.nstrips, g.Hc2 - 2, 4, 8, g.rb / 4);
   g.ntr = div_up(g.Hc2 - 2, g.rb / 4);
   const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);
   hipStream_t s = (hipStream_t)stream;
@@ -3335,7 +3363,10 @@ static int prolong2(const T* fc, const T* ec2, const T* f, T* out, const uint8_t
   g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;
   g.Hc2 = (Hc + 1) / 2; g.Wc2 = (Wc + 1) / 2; g.ldc2 = ldc2; g.bsc2 = bsc2;
   g.nstrips = div_up(W - 2, Ovl4<T>::S);
-  g.rb = pick_rb(B, g.nstrips, H - 2);
+  // (no taller tasks than the power-of-two choice: batched fp32 prolong2 at 1025^2 x 256 ran 41.7 -> 51.5 us with
+  // half the waves)
+  const int u2 = pick_rb(B, g.nstrips, H - 2) / 2;
+  g.rb = 2 * balanced_units(B, g.nstrips, (H - 1) / 2, 2, 4, u2, u2);
   g.ntr = div_up(H - 2, g.rb);
   const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);
   hipStream_t s = (hipStream_t)stream;
