@@ -39,12 +39,17 @@ constexpr int kHTS = 10;          // LDS table stride (9 weights + omega/d)
 // renamings) for the sweep+restriction of a stored iterate, 2 elsewhere (the longer body costs those kernels their
 // third wave per SIMD: 4097^2 fp64 sweep+restriction 133.4 -> 116.8 us at 6, prolongation+sweep 103.5 -> 114.2 us;
 // same-lease A/B, profiles/r04_hjac).  FEA_HS_UNROLL overrides both (lab builds).
-template <int MODE, bool ZERO>
+// the fp64 single-pattern prolongation+sweep: 6 steps per body held to 168 VGPRs (three waves per SIMD)
+template <typename T, bool MULTI, int MODE, bool RAW>
+constexpr bool hs_mode1_wide() {
+  return MODE == 1 && sizeof(T) == 8 && !MULTI && !RAW;
+}
+template <typename T, bool MULTI, int MODE, bool ZERO, bool RAW>
 constexpr int hs_unroll_steps() {
 #ifdef FEA_HS_UNROLL
   return FEA_HS_UNROLL;
 #else
-  return (MODE == 2 && !ZERO) ? 6 : 2;
+  return (MODE == 2 && !ZERO) || hs_mode1_wide<T, MULTI, MODE, RAW>() ? 6 : 2;
 #endif
 }
 
@@ -179,7 +184,8 @@ struct HSArgs {
 //   the middle row is formed one row later and three residual rows close a coarse row (k_mg_resid_restrict's
 //   expressions); the wave loads two more halo columns per side and a task owns rb/2 coarse rows.
 template <typename T, bool MULTI, bool ZERO, bool RAW, int NL, int MODE>
-__global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1))) void k_mg_hsweep_strip(HSArgs<T> g) {
   static_assert(MODE != 1 || !ZERO, "the prolongation variant corrects a stored iterate");
   constexpr int V = HVec<T>::V;
   constexpr int Q = V / 2;
@@ -612,7 +618,7 @@ __global__ __launch_bounds__(256) void k_mg_hsweep_strip(HSArgs<T> g) {
     }
   };
   // the loop body holds U steps (hs_unroll_steps), the remainder one by one
-  constexpr int U = hs_unroll_steps<MODE, ZERO>();
+  constexpr int U = hs_unroll_steps<T, MULTI, MODE, ZERO, RAW>();
   static_assert(U % PF == 0 && U % 2 == 0, "hsweep unroll: even, a multiple of the prefetch ring");
   int y = y0;
   for (; y + U - 1 <= y1; y += U) hs_unroll<U>([&](auto i) __attribute__((always_inline)) { step(y + decltype(i)::value, i); });
