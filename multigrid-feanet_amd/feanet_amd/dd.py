@@ -564,7 +564,7 @@ class DDSolver:
             # two-level launches on the distributed levels between the communication steps (same per-level
             # computations on the same local nodes, so the ghost validity of every step is unchanged)
             ok = lambda l: l >= 1 and l + 2 <= self.Ld
-            steps = pair_prolongations(pair_restrictions(steps, ok), ok)
+            steps = pair_prolongations(pair_restrictions(steps, ok), ok, finest_first=False)
         direct = None  # ("scatter", dst) folded into the next launch: it reads the coarse solution in place
         for si, st in enumerate(steps):
             if st[0] == "scatter" and self._scatter_direct(st, steps[si + 1] if si + 1 < len(steps) else None):

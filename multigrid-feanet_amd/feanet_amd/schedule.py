@@ -218,23 +218,49 @@ def pair_restrictions(steps, can_pair):
     return out
 
 
-def pair_prolongations(steps, can_pair):
+def pair_prolongations(steps, can_pair, finest_first=True):
     """Rewrite two consecutive recomputed-iterate prolongations (("prolong_sweep", l+1, OMDF, c, d), then
     ("prolong_sweep", l, OMDF, d, e)) into one ("prolong_sweep2", l, c, e) step — fea_mg_prolong2, bitwise
-    the two; the intermediate iterate d of level l+1 is then never stored — where can_pair(l) allows it."""
+    the two; the intermediate iterate d of level l+1 is then never stored — where can_pair(l) allows it.
+    Within a run of chained prolongations the FINEST levels pair first (the run is paired from its end): the
+    iterate a pair keeps out of HBM is the larger one there (C5, 1025^2 x 256: levels 2-1 paired, level 3 alone,
+    instead of 3-2 paired and level 1 alone).  finest_first=False pairs from the run's start (the coarsest levels
+    first: the domain decomposition keeps that, so the pair right under the agglomeration level reads the coarse
+    solution in place, DDSolver._scatter_direct)."""
+    ps = lambda st: st[0] == "prolong_sweep" and st[2] == OMDF
+    chained = lambda a, b: ps(a) and ps(b) and b[1] == a[1] - 1 and b[3] == a[4]
     out = []
     i = 0
-    ps = lambda st: st[0] == "prolong_sweep" and st[2] == OMDF
     while i < len(steps):
-        st = steps[i]
-        if i + 1 < len(steps) and ps(st) and ps(steps[i + 1]):
-            nx = steps[i + 1]
-            if nx[1] == st[1] - 1 and nx[3] == st[4] and can_pair(nx[1]):
-                out.append(("prolong_sweep2", nx[1], st[3], nx[4]))
-                i += 2
-                continue
-        out.append(st)
-        i += 1
+        if not ps(steps[i]):
+            out.append(steps[i])
+            i += 1
+            continue
+        j = i + 1  # the run steps[i:j] of chained prolongations
+        while j < len(steps) and chained(steps[j - 1], steps[j]):
+            j += 1
+        run, paired = steps[i:j], []
+        if finest_first:
+            k = len(run)
+            while k > 0:
+                if k >= 2 and can_pair(run[k - 1][1]):
+                    paired.append(("prolong_sweep2", run[k - 1][1], run[k - 2][3], run[k - 1][4]))
+                    k -= 2
+                else:
+                    paired.append(run[k - 1])
+                    k -= 1
+            paired.reverse()
+        else:
+            k = 0
+            while k < len(run):
+                if k + 1 < len(run) and can_pair(run[k + 1][1]):
+                    paired.append(("prolong_sweep2", run[k + 1][1], run[k][3], run[k + 1][4]))
+                    k += 2
+                else:
+                    paired.append(run[k])
+                    k += 1
+        out.extend(paired)
+        i = j
     return out
 
 
