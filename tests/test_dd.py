@@ -173,3 +173,31 @@ def test_partition_2d():
                 q1 = part.clevel(l + 1, r)
                 assert q.gr0 == 2 * q1.gr0 and q.Hloc == 2 * q1.Hloc - 1
         assert cols == list(range(1, W - 1))
+
+
+def test_rect_records_decompose_the_dd_copies():
+    """dd._rect_records (the fea_dd_copy_rects table behind the agglomeration's copies): the placement view pair
+    ([B, Pr, c, Pc, cc] strided views) becomes B * Pr * Pc rectangles of c x cc with the right addresses and pitches;
+    a row-slab run ([B, run]) one rectangle of B rows; views without a common unit-stride dimension are refused.
+    Checked by replaying the records with numpy on host tensors."""
+    import torch
+    from feanet_amd.dd import _rect_records
+    B, Pr, Pc, c, cc, ld = 2, 3, 4, 5, 6, 40
+    field = torch.zeros(B, Pr * c + 3, ld, dtype=torch.float64)
+    stage = torch.arange(Pr * Pc * B * c * cc, dtype=torch.float64).reshape(Pr * Pc, B, c, cc)
+    dst = field[:, 1:1 + Pr * c, 2:2 + Pc * cc].reshape(B, Pr, c, Pc, cc)
+    src = stage.view(Pr, Pc, B, c, cc).permute(2, 0, 3, 1, 4)
+    recs = _rect_records(dst, src)
+    assert recs.shape == (B * Pr * Pc, 6) and (recs[:, 4:] == [c, cc]).all()
+    flat_d, flat_s = field.view(-1).numpy(), stage.view(-1).numpy()
+    base_d, base_s, esz = field.data_ptr(), stage.data_ptr(), 8
+    for d0, s0, dld, sld, rows, cols in recs:
+        for r in range(rows):
+            o_d, o_s = (d0 - base_d) // esz + r * dld, (s0 - base_s) // esz + r * sld
+            flat_d[o_d:o_d + cols] = flat_s[o_s:o_s + cols]
+    assert torch.equal(dst, src)
+    run = torch.zeros(B, 50, dtype=torch.float32)
+    r2 = _rect_records(run[:, :20], run[:, 30:])
+    assert r2.shape == (1, 6) and list(r2[0, 2:]) == [50, 50, B, 20]
+    assert _rect_records(field[:, 1:4, 0:1].transpose(1, 2), field[:, 1:4, 2:3].transpose(1, 2)) is None
+

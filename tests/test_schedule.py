@@ -331,6 +331,29 @@ def test_level_pairing_equals_per_level(problem, groups, npairs):
     np.testing.assert_array_equal(out, ref)
 
 
+@pytest.mark.parametrize("finest_first", [True, False])
+def test_prolongation_pairing_order(finest_first):
+    """A run of three chained recomputed-iterate prolongations (levels 3, 2, 1): finest-first pairs 2-1 and leaves
+    level 3 alone (the single-GPU default: the larger iterate stays out of HBM), coarsest-first pairs 3-2 and leaves
+    level 1 (the domain decomposition's choice); both are the per-level V-cycle (oracle operators)."""
+    from feanet_amd.schedule import OMDF, pair_prolongations
+    n, L = 64, 6
+    rng = np.random.default_rng(7)
+    mg = orc.OracleMultigrid(n, "poisson", np.float64, levels=L)
+    mg.nu, mg.q2 = (1, 1), False
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    steps, end = vcycle_schedule(L, 1, 1, tail_from=4)
+    ps = [s for s in steps if s[0] == "prolong_sweep" and s[2] == OMDF]
+    assert [s[1] for s in ps] == [3, 2, 1]
+    paired = pair_prolongations(steps, lambda l: l + 2 < L, finest_first=finest_first)
+    pairs = [s[1] for s in paired if s[0] == "prolong_sweep2"]
+    singles = [s[1] for s in paired if s[0] == "prolong_sweep" and s[2] == OMDF]
+    assert (pairs, singles) == (([1], [3]) if finest_first else ([2], [1]))
+    ref = interpret(mg, steps, v, f)[0][end]
+    np.testing.assert_array_equal(interpret(mg, paired, v, f)[0][end], ref)
+
+
 @pytest.mark.parametrize("k", [1, 2, 5, 20, 31, 32, 33, 64, 100, 1000])
 def test_vcycle_blocks_cover_k(k):
     """vcycle(k) replays blocks of GRAPH_CYCLES joined cycles plus one block of the rest (pipe_blocks), and
