@@ -27,13 +27,11 @@ constexpr int kHMaxLayers = 3;    // HNet(nb_layers=3) (M-FEANet-mg_test.ipynb:2
 constexpr int kHPrefetch = FEA_HSWEEP_PF;
 static_assert(kHPrefetch == 1 || kHPrefetch == 2, "hsweep prefetch of 1 or 2 rows");
 constexpr int kHTS = 10;          // LDS table stride (9 weights + omega/d)
-// FEA_HS_WRELOAD: the stencil / HNet / transfer weights (up to 46 doubles: more than the SGPR file holds beside
-// the kernel's addresses) are re-read with scalar loads at every row step instead of being hoisted once — hoisted,
-// the compiler parks them in VGPR lanes and pays a v_readlane per 32-bit half at every use (~95 VALU per step
-// of the fp64 sweep+restriction, as many as its FMAs).
-#ifndef FEA_HS_WRELOAD
-#define FEA_HS_WRELOAD 1
-#endif
+// Weights: the stencil / HNet / transfer weights (up to 46 doubles: more than the SGPR file holds beside the
+// kernel's addresses) are re-read with scalar loads at every row step, stage by stage, each stage's loads held
+// behind an empty asm that "changes" their offset — hoisted out of the loop, or loaded all at the step's start,
+// the compiler parks them (and with them the loop's other scalars) in VGPR lanes and pays a v_readlane per 32-bit
+// half at every use (~95 VALU per step of the fp64 sweep+restriction, as many as its FMAs).
 
 // steps per loop body: 6 (the 3-row windows' period x the 2-slot ring: the window rotations become register
 // renamings) for the sweep+restriction of a stored iterate, 2 elsewhere (the longer body costs those kernels their
@@ -161,7 +159,7 @@ struct HSArgs {
   int H, W, ld;
   long long bs;
   int nstrips, ntr, rb;
-  int zmask;  // 0 (FEA_HS_WRELOAD: an offset the compiler cannot fold)
+  int zmask;  // 0 (the weight loads' offset the compiler cannot fold)
   // MODE 1 (prolongation + correction first): the sweep's iterate is x = u + w1 P(ec)
   const T* ec;
   const uint8_t* pidc;
@@ -375,23 +373,31 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   auto step = [&](int y, auto pos_c) __attribute__((always_inline)) {
     constexpr int SL = decltype(pos_c)::value % PF;
     constexpr bool ODD = decltype(pos_c)::value & 1;  // y odd (y0 is even)
-#if FEA_HS_WRELOAD
-    {
-      const int z = y & g.zmask;  // 0 at run time, unknown to the compiler: the loads stay in the step
+    int z = y & g.zmask;  // 0 at run time, unknown to the compiler: the weight loads stay in the step
+    // stage barrier: z is "changed" by an empty asm, so the weight loads after it cannot be hoisted above it —
+    // each stage's weights are loaded just before the stage and die after it (one stage's worth of SGPRs live).
+    // fp64 only: 4097^2 MG-HJac 486 -> 456 us (prolongation+sweep 101.6 -> 96.7 us, level 1 38.3 -> 30.5 us);
+    // the fp32 129^2 cycle ran 1 % slower with them (profiles/r04_hjac/staged_weights_ab.txt)
+    auto stage_ks = [&]() __attribute__((always_inline)) {
+      if constexpr (sizeof(T) == 8) asm volatile("" : "+s"(z));  // (fp32: measured without the barriers)
       if constexpr (!MULTI) {
 #pragma unroll
-        for (int d = 0; d < 9; ++d) {
-          ks[d] = cload(g.ktab, z + d);
-          if constexpr (MODE != 0) t2[d] = cload(MODE == 1 ? g.ptab : g.rtab, z + d);
-        }
+        for (int d = 0; d < 9; ++d) ks[d] = cload(g.ktab, z + d);
         om = cload(g.omd, z);
       }
+    };
+    auto stage_t2 = [&]() __attribute__((always_inline)) {
+      if constexpr (sizeof(T) == 8) asm volatile("" : "+s"(z));  // (fp32: measured without the barriers)
+      if constexpr (!MULTI && MODE != 0) {
 #pragma unroll
-      for (int l = 0; l < NL; ++l)
+        for (int d = 0; d < 9; ++d) t2[d] = cload(MODE == 1 ? g.ptab : g.rtab, z + d);
+      }
+    };
+    auto stage_hk = [&](int l) __attribute__((always_inline)) {
+      if constexpr (sizeof(T) == 8) asm volatile("" : "+s"(z));  // (fp32: measured without the barriers)
 #pragma unroll
-        for (int d = 0; d < 9; ++d) hk[l][d] = cload(g.hw, z + l * 9 + d);
-    }
-#endif
+      for (int d = 0; d < 9; ++d) hk[l][d] = cload(g.hw, z + l * 9 + d);
+    };
     // this step's rows (their loads were issued two steps ago), then the slot's refill for step y+2
     T uy[V], fy1[V], raw[V], fres[V], uout[V];
     int py[V], pout[V];
@@ -407,6 +413,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     }
     fill(SL, y + PF);  // (rows past the task's last are clamped into the frame: loaded, never used)
     if constexpr (MODE == 1) {
+      stage_t2();
       // x(y) = u(y) + w1 P(ec) on the interior (correct_even / correct_odd of k_mg_prolong)
       const bool yin = y >= 1 && y <= H - 2;
 #pragma unroll
@@ -435,6 +442,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
       P2 = hpwin<V>(py);
     }
     // j and d_0 of row y-1
+    stage_ks();
     const int yj = y - 1;
     const bool rin = yj >= 1 && yj <= H - 2, rgr = yj >= 0 && yj <= H - 1;
     T d0[V], jv[V];
@@ -494,6 +502,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     // d_l of row y-1-l from the d_(l-1) window of rows y-1-l-1 .. y-1-l+1
 #pragma unroll
     for (int l = 1; l <= NL; ++l) {
+      stage_hk(l - 1);
       const int yl = y - 1 - l;
       const bool lin = yl >= 1 && yl <= H - 2;
       T dl[V];
@@ -538,6 +547,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
       }
       // residual row yr = yo - 1 (fea_mg_residual_restrict's resid), then the restriction of its coarse row
       const int yr = yo - 1;
+      stage_ks();
       if (yr >= rc0 + 1) {
         T r[V + 1];
         const T(&fr)[V] = fres;
@@ -568,6 +578,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
           r[k] = fr[k] - acc;
         }
         r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+        stage_t2();
         if constexpr (((ODD ? 1 : 0) + NL) % 2 == 0) {  // row 2I (yr = y - 2 - NL)
 #pragma unroll
           for (int k = 0; k <= V; ++k) Rb[k] = r[k];
