@@ -42,6 +42,7 @@ struct HTailArgs {
   int Ht, Wt, nlev, ld_t;
   long long bs_t;
   int ntab, nl, nu1, nu2;
+  int zmask;  // 0 (staged weight loads)
 };
 
 __host__ __device__ inline int htail_n(int n0, int k) { return ((n0 - 1) >> k) + 1; }
@@ -71,21 +72,37 @@ struct HTail {
   const T* hk;   // nl x 9
   T ks[9], rs[9], ps[9], om0;
   int tid;
+  mutable int z;  // 0; "changed" by an empty asm at every pass (stage()): the weights are re-read per pass
+
+  template <typename U>
+  __device__ __forceinline__ static U kload(const U* p, int i) {  // scalar read-only load (constant space)
+    return ((const __attribute__((address_space(4))) U*)p)[i];
+  }
+  // fp64 single-pattern: each pass re-reads its weights (after the barrier, hoisted to the pass's start) instead
+  // of keeping all 28 in SGPRs the compiler parks in VGPR lanes
+  static constexpr bool kStage = !MULTI && sizeof(T) == 8;
+  __device__ __forceinline__ void stage() const {
+    if constexpr (kStage) asm volatile("" : "+s"(z));
+  }
 
   __device__ __forceinline__ T kw(const uint8_t* pk, int i, int d) const {
     if constexpr (MULTI) return ktb[pk[i] * kHTailTS + d];
+    else if constexpr (kStage) return kload(a.ktab, z + d);
     return ks[d];
   }
   __device__ __forceinline__ T omk(const uint8_t* pk, int i) const {
     if constexpr (MULTI) return ktb[pk[i] * kHTailTS + 9];
+    else if constexpr (kStage) return kload(a.omd, z);
     return om0;
   }
   __device__ __forceinline__ T rw(const uint8_t* pk, int i, int d) const {
     if constexpr (MULTI) return rtb[pk[i] * kHTailTS + d];
+    else if constexpr (kStage) return kload(a.rtab, z + d);
     return rs[d];
   }
   __device__ __forceinline__ T pw(const uint8_t* pk, int i, int d) const {
     if constexpr (MULTI) return ptb[pk[i] * kHTailTS + d];
+    else if constexpr (kStage) return kload(a.ptab, z + d);
     return ps[d];
   }
   // (K x)(i) at an interior node of a W-wide level (taps in row-major order, the weight by the tap node's pattern)
@@ -104,7 +121,7 @@ struct HTail {
   }
   // HNet layer l (cross-correlation, zero padding) at an interior node
   __device__ __forceinline__ T conv(const T* d, int l, int i, int W) const {
-    const T* h = hk + l * 9;
+    const T* h = hk + l * 9;  // (LDS)
     const int n = i - W, s = i + W;
     T acc = h[0] * d[n - 1];
     acc += h[1] * d[n];
@@ -131,6 +148,7 @@ struct HTail {
   // one HRelax sweep of u in place (A, B: scratch fields of >= H*W)
   __device__ void hrelax(int H, int W, const T* f, T* u, const uint8_t* pk, T* A, T* B) const {
     const int n = H * W;
+    stage();
     for (int i = tid; i < n; i += kHTailThreads) {
       T j = T(0), d = T(0);
       if (inner(i, H, W)) {
@@ -177,6 +195,7 @@ struct HTail {
   __device__ void restrict_(int H, int W, const T* f, const T* u, const uint8_t* pk, T* fc) const {
     const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
     const int n = (Hc - 2) * (Wc - 2);
+    stage();
     for (int t = tid; t < n; t += kHTailThreads) {
       const int I = divw(t, Wc - 2) + 1, J = t - (I - 1) * (Wc - 2) + 1;
       T r[9];
@@ -217,6 +236,7 @@ struct HTail {
   __device__ void prolong_add(int H, int W, T* u, const T* e, const uint8_t* pc) const {
     const int Wc = (W + 1) / 2;
     const T w1 = a.w1;
+    stage();
     for (int i = tid; i < H * W; i += kHTailThreads) {
       if (!inner(i, H, W)) continue;
       const int y = divw(i, W), x = i - y * W;
@@ -265,7 +285,7 @@ __global__ __launch_bounds__(kHTailThreads) void k_hjac_tail(HTailArgs<T> a) {
     const int r = i / Wt, c = i - r * Wt;
     fs[i] = fg[(long long)(r + 1) * a.ld_t + c];
   }
-  HTail<T, MULTI> t{a, ktb, rtb, ptb, hk, {}, {}, {}, T(0), tid};
+  HTail<T, MULTI> t{a, ktb, rtb, ptb, hk, {}, {}, {}, T(0), tid, a.zmask};
   if constexpr (!MULTI) {
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
