@@ -177,6 +177,43 @@ def time_join_in_cycle(s, k):
     return with_join - without
 
 
+def time_fine_launch_in_cycle(s, reps=5):
+    """Solvers whose cycles are not joined (the learned smoother's MG-HJac schedule): every launch of the V-cycle
+    plan timed INSIDE the cycle — eager replays of the plan with a HIP event on the solver's stream between
+    consecutive launches — and the slowest finest-level launch returned as (kernel name, seconds per launch,
+    algorithmic bytes per launch).  Algorithmic bytes per fine node / coarse node: hsweep u, f -> u' (3 es);
+    hsweep + restriction also writes f_c (es per coarse node); prolongation + hsweep also reads e_c (es)."""
+    from feanet_amd import _lib
+    st = torch.cuda.current_stream()
+    L0, L1 = s.levels[0], s.levels[1]
+    f0 = L0.f.data_ptr()
+    es = torch.finfo(s.dtype).bits // 8
+    pb = 1 if L0.pid is not None else 0
+    nodes = L0.B * (L0.H - 2) * (L0.W - 2)
+    cnodes = L1.B * (L1.H - 2) * (L1.W - 2)
+    fslot = {"mg_hsweep": 2, "mg_hsweep_restrict": 2, "mg_prolong_hsweep": 3, "mg_sweep": 1,
+             "mg_sweep_restrict": 1, "mg_prolong_sweep": 2}
+    cbytes = {"mg_hsweep": 0, "mg_sweep": 0, "mg_hsweep_restrict": es, "mg_sweep_restrict": es,
+              "mg_prolong_hsweep": es + pb, "mg_prolong_sweep": es + pb}
+    acc = {}
+    for _ in range(reps):
+        plan, end = s._plan(s._state)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
+        ev[0].record(st)
+        for i, (name, args) in enumerate(plan):
+            _lib.call(name, s.dtype, *args, st.cuda_stream)
+            ev[i + 1].record(st)
+        s._state = end
+        ev[-1].synchronize()
+        for i, (name, args) in enumerate(plan):
+            if name in fslot and args[fslot[name]] == f0:
+                acc.setdefault((i, name), []).append(ev[i].elapsed_time(ev[i + 1]) * 1e-3)
+    if not acc:
+        return None
+    (i, name), ts = max(acc.items(), key=lambda kv: sum(kv[1]))
+    return "fea_" + name, sum(ts) / len(ts), (3 * es + pb) * nodes + cbytes[name] * cnodes
+
+
 def load_traffic(kernel_key):
     """Measured HBM bytes per launch from a rocprofv3 PMC record (profiles/pmc_traffic.json), only if it was
     taken on the kernel source this run executes (SHA-256 stamp of csrc/framed_ops.hip); else (None, why)."""
@@ -315,12 +352,35 @@ def dd_domain(P, n0):
     return n0 * P, n0
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the same command line under
+    torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a CHILD process — nothing here has
+    touched the GPU, and the process is not replaced (no exec) — forward its one JSON line to stdout (anything
+    else it printed there goes to stderr) and return its exit status."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n} without a launcher: {' '.join(cmd)}")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = r.stdout.splitlines()
+    recs = [ln for ln in lines if ln.startswith("{")]
+    for ln in lines:
+        if not ln.startswith("{"):
+            log(ln)
+    if recs:
+        print(recs[-1], flush=True)
+    if r.returncode == 0 and len(recs) != 1:
+        log(f"[bench] expected one JSON line from rank 0, got {len(recs)}")
+        return 1
+    return r.returncode
+
+
 def main():
-    # stdout carries exactly ONE line, the JSON record: everything else a library writes to fd 1
-    # (RCCL prints its version banner there when the communicator comes up) goes to stderr
-    json_out = os.fdopen(os.dup(1), "w")
-    sys.stdout.flush()
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -354,6 +414,18 @@ def main():
                     help="torch.distributed backend (gloo: multi-process rehearsal on one GPU, host-staged)")
     ap.add_argument("--kernel-reps", type=int, default=50)
     args = ap.parse_args()
+
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_ws is not None and int(env_ws) != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_ws} ranks; pass --gpus "
+                 f"{env_ws} (or run without a launcher: bench.py --gpus N starts N ranks itself)")
+    # stdout carries exactly ONE line, the JSON record: everything else a library writes to fd 1
+    # (RCCL prints its version banner there when the communicator comes up) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     mode = args.mode or ("dd" if ws > 1 else "single")
@@ -446,22 +518,41 @@ def main():
     jt = time_join_in_cycle(s, min(args.steps, 200)) if mode == "single" else None
     jsrc = ("HIP events in the solver's stream, eager replays of vcycle(K): [previous launch + join] minus "
             "[previous launch] per cycle")
-    if jt is None and "fea_mg_cycle_join" in fine:
+    dom = None
+    if jt is None and mode == "single" and not s._joinable():
+        dom = time_fine_launch_in_cycle(s)  # no join in this schedule: its own slowest fine-level launch
+    if dom is not None:
+        name, r_t, r_bytes = dom
+        rkern = (f"{name} (fine level {L0.H}x{L0.W} {args.dtype}; the slowest launch of the cycle, which joins no "
+                 f"cycles)")
+        tkey, jsrc = None, ("HIP events on the solver's stream between consecutive launches of eager replays of the "
+                            "V-cycle plan")
+    elif jt is None and "fea_mg_cycle_join" in fine:
         jt = fine["fea_mg_cycle_join"][0]
         jsrc = "HIP events, back-to-back launches of fea_mg_cycle_join on the level-0 buffers"
-    if jt is not None:
+    if dom is None and jt is not None:
         jbytes = fine["fea_mg_cycle_join"][1] if "fea_mg_cycle_join" in fine else None
         jt = max_over_ranks(jt, ws)
         rkern = f"fea_mg_cycle_join (fine level {L0.H}x{L0.W} {args.dtype}: post-sweep of cycle k + pre-sweep, " \
                 f"residual and restriction of cycle k+1 in one pass)"
         r_t, r_bytes, tkey = jt, jbytes, "mg_cycle_join_f64_4097"
-    else:
+    elif dom is None:
         rkern, r_t, r_bytes, tkey, jsrc = (f"fea_mg_sweep ({L0.H}x{L0.W} {args.dtype})", kt, kbytes,
                                            "mg_sweep_f64_4097", "HIP events, back-to-back launches")
     achieved = r_bytes / r_t / 1e9
     traffic, tsrc = load_traffic(tkey) if (mode == "single" and metric_cfg) else (None, None)
     ns_traffic, ns_src = load_traffic("mg_sweep_f64_4097") if (mode == "single" and metric_cfg) else (None, None)
     vbytes = s.bytes_per_vcycle(args.steps) if mode == "single" else None
+    dd_mode = None
+    if mode == "dd":  # the path the timed cycles actually took (a refused capture falls back on every rank)
+        captured = bool(getattr(s.comm, "capturable", False) and s._capture_ok and s.use_graph)
+        dd_mode = {"cycle_graphs": "captured (kernels + RCCL calls, one HIP graph per block of up to "
+                                   f"{s.GRAPH_CYCLES} cycles)" if captured else "segments (one HIP graph per kernel "
+                                   "segment between communication steps)",
+                   "split_join": bool(s.split_join and captured), "overlap_l0": bool(s.overlap_l0),
+                   "backend": args.backend}
+        parallelism += (f"; cycles {'captured whole' if captured else 'in kernel segments'}, split_join "
+                        f"{dd_mode['split_join']}, overlap_l0 {dd_mode['overlap_l0']}")
 
     rec = {
         "metric": METRIC,
@@ -478,7 +569,8 @@ def main():
         "data": ("synthetic (seeded Gaussian rhs, zero initial guess)" if rhs == "randn" else
                  "synthetic (nodal sources from the six Data/RHS/generate_rhs.py families, seeded, FNet applied; "
                  "zero initial guess)"),
-        "config": {"workload": workload, "mode": mode, "batch": B, "levels": s.L, "parallelism": parallelism},
+        "config": {"workload": workload, "mode": mode, "batch": B, "levels": s.L, "parallelism": parallelism,
+                   **({"dd_mode": dd_mode} if dd_mode else {})},
         "roofline": {"bound": "hbm", "kernel": rkern,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": r_t * 1e6,

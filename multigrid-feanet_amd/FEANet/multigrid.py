@@ -195,7 +195,12 @@ class MultiGrid(nn.Module):
         """The MultigridSolver of this batch shape, built once.  An optimizer step changes R / P in place
         (their _version moves): the new values are copied into the solver's resident tables
         (MultigridSolver.set_transfer) instead of rebuilding it, so level buffers, pattern maps and captured
-        graphs are reused across training steps; the ratios w are read back to the host only when they change."""
+        graphs are reused across training steps; the ratios w are read back to the host only when they change.
+
+        Changes are detected by (data_ptr, _version) of R, P and w: in-place updates must go through tracked
+        tensor ops (optimizer steps, `with torch.no_grad(): w.copy_(...)`) or reassign the parameter.  Writes
+        through `.data` (e.g. `mg.w.data.fill_(...)`) do not move `_version` and are NOT seen: call
+        `self._solver_ver = None` after such a write (the next iterate then copies all three)."""
         from feanet_amd.solver import MultigridSolver
         key = (x.shape[0], x.dtype, x.device)
         ver = self._transfer_version()
@@ -206,7 +211,7 @@ class MultiGrid(nn.Module):
                                            w=(float(self.w[0]), float(self.w[1])))
             self._solver_key = key
         elif ver != self._solver_ver:
-            old = self._solver_ver
+            old = self._solver_ver or (None, None, None)
             self._solver.set_transfer(R=self.conv.net.weight[0] if ver[0] != old[0] else None,
                                       P=self.deconv.net.weight[:, 0] if ver[1] != old[1] else None,
                                       w=self.w if ver[2] != old[2] else None)

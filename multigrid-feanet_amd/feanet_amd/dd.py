@@ -840,7 +840,14 @@ class DDSolver:
         gaps between its kernel segments and ~one host graph launch per block.  Each block runs eagerly once
         (plans, communicator set-up), is captured the second time and replayed after that.  A communicator whose
         operations cannot be captured (capture raises) turns this off for the solver; it then runs the
-        segment-wise path."""
+        segment-wise path.
+
+        The decision is collective: a capture records the communicator's calls without running them, so after
+        every capture the ranks agree (one all-reduce, outside the graph) whether ALL of them captured; if any
+        refused, every rank discards its graphs and runs the segment-wise path from that block on — the same
+        calls in the same order on every rank, so no message is left unmatched.  Only capture failures count as
+        a refusal (CUDA/HIP graph or stream-capture errors); any other error (e.g. an invalid kernel argument)
+        propagates."""
         i = 0
         while i < len(keys):
             key = keys[i]
@@ -859,20 +866,35 @@ class DDSolver:
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(stream)
+                ok = True
                 try:
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         self._run_chunks(block, captured=True)
-                except RuntimeError:  # capture refused: this rank runs the segment-wise path from now on
+                except RuntimeError as e:
+                    if not _is_capture_error(e):
+                        raise
+                    ok = False
+                    g = None
                     torch.cuda.synchronize(self.device)
+                stream.wait_stream(s)
+                if not self._all_ranks_ok(ok):  # some rank refused: every rank leaves the captured path
                     self._capture_ok = False
+                    self._graphs = {k: v for k, v in self._graphs.items() if k[0] != "cap"}
                     self._run_chunks(keys[i:], captured=False)
                     return
-                stream.wait_stream(s)
                 self._graphs[gkey] = g
                 g.replay()
             else:
                 g.replay()
             i += n
+
+    def _all_ranks_ok(self, ok):
+        """True iff `ok` holds on every rank (one all-reduce of the refusal count through the communicator)."""
+        if getattr(self.comm, "world", 1) <= 1:
+            return ok
+        bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=self.device)
+        bad = self.comm.allreduce_sum(bad)
+        return float(bad.item()) == 0.0
 
     def _run_chunks(self, keys, captured=False):
         """Issue the chunks' kernel segments and communication steps in order on the current stream; captured:
@@ -987,6 +1009,19 @@ class DDSolver:
         return torch.sqrt(n2)
 
 
+def _is_capture_error(e):
+    """Does this exception say that stream capture was refused (rather than that a call was wrong)?  HIP's
+    stream-capture error codes are 900-908 (hipErrorStreamCapture*, hipErrorCapturedEvent); torch and RCCL name
+    the capture in their messages.  The C ABI's FEA_EINVAL ('invalid arguments') is never one."""
+    msg = str(e)
+    if "invalid arguments" in msg:
+        return False
+    if any(f"hipError_t {c})" in msg for c in range(900, 909)):
+        return True
+    low = msg.lower()
+    return "captur" in low or "graph" in low
+
+
 def ctypes_addr(arr):
     import ctypes
     return ctypes.addressof(arr)
@@ -1074,10 +1109,12 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.gpu = dist.get_backend(group) == "nccl"
-        # DDSolver captures whole cycles (kernels + RCCL calls) in HIP graphs only where asked: RCCL calls are
-        # stream-capturable, but a multi-rank capture cannot be rehearsed on one GPU (FEANET_DD_CAPTURE=1)
+        # DDSolver captures whole cycles (kernels + RCCL calls) in HIP graphs by default on RCCL (host issue 4-5 us
+        # per cycle instead of 42-52, no graph-launch gaps between segments); if any rank's capture is refused,
+        # all ranks fall back to one graph per kernel segment (DDSolver._vcycle_captured).  FEANET_DD_CAPTURE=0
+        # turns it off.
         self.capturable = self.gpu and capture if capture is not None else (
-            self.gpu and os.environ.get("FEANET_DD_CAPTURE", "0") == "1")
+            self.gpu and os.environ.get("FEANET_DD_CAPTURE", "1") != "0")
 
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])

@@ -376,7 +376,13 @@ class MultigridSolver:
         resident tables IN PLACE on the current stream: the launch plans and captured HIP graphs hold the tables'
         addresses, so they stay valid and nothing is reallocated or recaptured.  The ratios are passed by value
         into the launches, so new ratios (w != the current ones) drop the plans and graphs instead; the level
-        buffers are kept either way."""
+        buffers are kept either way.
+
+        A solver resting in the pipelined state (after vcycle) has not stored its last cycle's end iterate: it
+        is recomputed from the pre-smoothed iterate and the level-1 correction with the CURRENT P (_collapse).
+        So that state is collapsed first, with the old tables, before any of them changes."""
+        if R is not None or P is not None or w is not None:
+            self._collapse()
         for src, dst, name in ((R, self.rtab, "R"), (P, self.ptab, "P")):
             if src is None:
                 continue
@@ -388,7 +394,6 @@ class MultigridSolver:
         if w is not None:
             w = [float(x) for x in (w.detach().cpu().tolist() if torch.is_tensor(w) else w)]
             if (w[0], w[1]) != self.w:
-                self._collapse()  # the pipelined state was built with the old ratios' plans
                 self.w = (w[0], w[1])
                 self._plans.clear()
                 self._graphs.clear()

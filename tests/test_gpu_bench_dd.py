@@ -40,3 +40,21 @@ def test_bench_dd_line_parity(ranks, grid):
     assert par["bitwise_equal"] and par["max_abs_diff"] == 0.0, par
     base = rec["single_gpu_same_grid"]
     assert base["ms_per_step"] > 0 and base["workload"].startswith("1025x1025")
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts the two ranks itself (torch.distributed.run as a child
+    process), forwards rank 0's one JSON line and records the decomposition mode it ran."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--backend", "gloo", "--global-n", "1024", "--kernel-reps", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["mode"] == "dd"
+    assert rec["dd_parity"]["bitwise_equal"], rec["dd_parity"]
+    dm = rec["config"]["dd_mode"]
+    assert dm["backend"] == "gloo" and dm["cycle_graphs"].startswith("segments")  # gloo is never captured

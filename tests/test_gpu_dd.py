@@ -252,7 +252,7 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph, m
     def run(r):
         try:
             fake.tls.rank = r
-            comm = TorchComm(dist=fake)
+            comm = TorchComm(dist=fake, capture=False)  # the segment-wise path (the fake's ops are host-side)
             assert comm.gpu and comm.rank == r
             # each rank on its own (non-default) stream, as each process of a real run: no rank's work goes to
             # the legacy default stream, which would synchronise with (and break) another rank's graph capture
@@ -322,3 +322,53 @@ def test_dd_captured_cycles_match_segments(P, grid, rank, n):
             assert any(v is not None for v in s._graphs.values())
     for a, b in zip(outs[1:], outs[:1] * 2):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("refuse", ["self", "peer", "einval"])
+def test_dd_capture_refusal_is_collective(refuse):
+    """The captured path's fallback (DDSolver._vcycle_captured): a capture refused on this rank ('self': the
+    communicator raises a stream-capture error inside the capture) or on another rank ('peer': this rank
+    captures, the agreement all-reduce reports one refusal) drops EVERY rank to the segment-wise path, with the
+    cycles' results bitwise those of that path; an error that is not a capture refusal ('einval') propagates."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from tools.dd_projection import PackComm
+    from feanet_amd.dd import DDSolver
+    P, grid, rank, n = 4, (2, 2), 1, 512
+    g = torch.Generator(device="cuda")
+    g.manual_seed(77)
+    f = torch.randn(1, 1, n + 1, n + 1, device="cuda", dtype=torch.float64, generator=g)
+
+    class Refusing(PackComm):
+        world = 2
+
+        def exchange_many(self, s, items, wait=True, packed=False):
+            if torch.cuda.is_current_stream_capturing():
+                if refuse == "self":
+                    raise RuntimeError("operation not permitted when stream is capturing")
+                if refuse == "einval":
+                    raise RuntimeError("feanet_amd: fea_dd_copy_blocks failed (invalid arguments)")
+            return super().exchange_many(s, items, wait, packed)
+
+        def allreduce_sum(self, t):
+            return t + 1 if refuse == "peer" else t
+
+    outs = []
+    for comm in (PackComm(), Refusing()):
+        comm.capturable = isinstance(comm, Refusing)
+        s = DDSolver(n, n, rank, P, comm=comm, agglomerate=2, grid=grid)
+        s.set_rhs(f)
+        s.load()
+        if refuse == "einval" and comm.capturable:
+            s.vcycle(3)  # eager once
+            with pytest.raises(RuntimeError, match="invalid arguments"):
+                s.vcycle(3)
+            return
+        for k in (1, 3, 3, 3, 2):
+            s.vcycle(k)
+        torch.cuda.synchronize()
+        if comm.capturable:
+            assert not s._capture_ok and not any(k[0] == "cap" for k in s._graphs)
+        L0 = s.local.levels[0]
+        outs.append(L0.view(L0.buf(s._state)).clone())
+    assert torch.equal(outs[0], outs[1])

@@ -880,6 +880,45 @@ def test_pipelined_state_semantics():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("what", ["P", "R", "w", "RP"])
+def test_set_transfer_keeps_pipelined_iterate(what):
+    """set_transfer on a solver resting in the pipelined state (its last end iterate not stored, recomputed with
+    the prolongation tables on demand): the iterate the finished cycles produced is kept — solution() after the
+    call equals solution() before it, bitwise, whether or not it had been materialised — and the next cycles run
+    with the new tables (they equal a solver built with them from that iterate)."""
+    from feanet_amd.solver import MultigridSolver
+    from feanet_amd import mesh_setup as ms
+    n, B = 128, 1
+    rng = np.random.default_rng(8)
+    f = torch.from_numpy(rng.standard_normal((B, 1, n + 1, n + 1))).cuda()
+    lin = ms.linear_transfer_kernel().reshape(1, 3, 3)
+    R2 = lin / 4 * 1.1 if "R" in what else None
+    P2 = lin * 0.9 if "P" in what else None
+    w2 = (0.9, 1.2) if what == "w" else None
+    for peek in (False, True):
+        s = MultigridSolver(n, dtype=torch.float64, batch=B)
+        s.set_rhs(f=f)
+        s.load()
+        s.vcycle(2)
+        before = s.solution().clone() if peek else None
+        if not peek:  # reference value from a twin solver that never changes its tables
+            t = MultigridSolver(n, dtype=torch.float64, batch=B)
+            t.set_rhs(f=f)
+            t.load()
+            t.vcycle(2)
+            before = t.solution().clone()
+        s.set_transfer(R=R2, P=P2, w=w2)
+        assert torch.equal(s.solution(), before), (what, peek)
+        s.vcycle(2)
+        after = s.solution()
+        ref = MultigridSolver(n, dtype=torch.float64, batch=B)
+        ref.set_transfer(R=R2, P=P2, w=w2)
+        ref.set_rhs(f=f)
+        ref.load(before)
+        ref.vcycle(2)
+        assert torch.equal(after, ref.solution()), (what, peek)
+
+
 def test_step_runs_unjoined_plan(monkeypatch):
     """step() (MultiGrid.Step / iterate, one cycle from a loaded iterate, read at once) launches exactly the
     unjoined plan — no cycle join, no discarded pipelined pre-smooth — also right after a pipelined
