@@ -267,6 +267,7 @@ struct MgArgs {
   int rlo, rhi;      // row range of the residual norm
   int clo, chi;      // column range of the residual norm
   int nt;            // 1: nontemporal stores (level larger than FEANET_NT_BYTES); 2: also loads (sweep, join)
+  int rev;           // decode_task_lin: deal the launch's tasks in reverse order (last task first)
   // cycle join over up to 4 rectangles (nrect > 0; a domain-decomposed rank's border strips, then its interior):
   // rectangle r = coarse rows [rI0[r], rI1[r]) x fine columns [rc0[r], rc1[r]) (odd bounds, coarse column J owned
   // with its fine columns 2J-1, 2J), its nstrips rns[r], its row tasks rnt[r]; the launch's tasks per sample are
@@ -299,10 +300,17 @@ __device__ __forceinline__ TaskId decode_task(int nstrips, int ntr) {
 // four (row task, strip) pairs of one sample instead of four strips of one row task, so no wave slot is
 // left empty (5 strips in two 4-wave groups idled 3 of 8 slots).  Workgroups never mix samples (the
 // fused norm partials stay per sample); only a sample's last workgroup may hold idle waves.
-__device__ __forceinline__ TaskId decode_task_lin(int nstrips, int ntr) {
+// the launch's logical block: XCD-remapped (each XCD a contiguous band), in reverse when `rev` (every XCD then
+// walks its band from the end)
+__device__ __forceinline__ int lin_block(int rev) {
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  return rev ? (int)gridDim.x - 1 - bid : bid;
+}
+
+__device__ __forceinline__ TaskId decode_task_lin(int nstrips, int ntr, int rev = 0) {
   const int per = ntr * nstrips;
   const int wpb = (per + kWaves - 1) / kWaves;  // workgroups per sample
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = lin_block(rev);
   TaskId id;
   id.b = bid / wpb;
   // the wave index is wave-uniform: keep the task coordinates in scalar registers
@@ -322,7 +330,7 @@ __device__ __forceinline__ TaskId decode_task_lin(int nstrips, int ntr) {
 template <typename T>
 __device__ __forceinline__ void norm_partial(const MgArgs<T>& g, double ssq) {
   ssq = wave_sum(ssq);
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = lin_block(g.rev);  // the slot of the block's tasks, whatever order they were dealt in
   if (lane_id() == 0) g.part[(long long)bid * kWaves + (threadIdx.x >> 6)] = ssq;
 }
 
@@ -2633,7 +2641,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
   JoinTask jt;
   bool valid;
   if (g.nrect == 0) {
-    const TaskId id = decode_task_lin(g.nstrips, g.ntr);
+    const TaskId id = decode_task_lin(g.nstrips, g.ntr, g.rev);
     valid = id.valid;
     jt.b = id.b;
     jt.t = id.t;
@@ -3149,6 +3157,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     join_config<T>(B, H, W, g);                                                                              \
     if (g.nt && bs * (long long)sizeof(T) > nt_load_bytes()) g.nt = 2;                                         \
+    if (getenv("FEA_LAB_JREV")) { static int flip = 0; g.rev = flip = !flip; }                                \
     g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
     hipStream_t s = (hipStream_t)stream;                                                                     \

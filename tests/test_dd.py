@@ -103,16 +103,16 @@ def test_default_agglomeration():
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_c4_agglomeration_level_is_the_measured_best(P):
     """C4 (8193^2 over the bench's 2x1 / 2x2 / 4x2 blocks): the default agglomeration level is the one the
-    per-rank projection chose — Ld = 4 (the 513^2 level): fastest at every rank count against Ld = 3, 5, 6
+    per-rank projection chose.  Round 3 (segment graphs): Ld = 4 (the 513^2 level), fastest at every rank count against Ld = 3, 5, 6
     (tools/dd_projection.py, profiles/r03_dd/dd_projection.txt: 8 ranks 151.8 us vs 158.5 / 155.9 / 154.7), and
     with the round-3 two-level launches within the run-to-run spread of Ld = 3 / 5 at 4 and 8 ranks
-    (profiles/r03_dd/dd_projection_paired.txt: 134.0 vs 135.8 / 135.7 us at 8 ranks).  Round 4: with the RCCL
-    default (a graph per kernel segment) Ld = 4 stays ahead at 8 ranks (123.7 vs 126.0 us); whole-cycle capture
-    (opt-in for RCCL) would favour Ld = 5 at 2 and 4 ranks (270.5 / 161.8 vs 287.9 / 170.3 us, level at 8:
-    profiles/r04_dd/dd_projection.txt)."""
+    (profiles/r03_dd/dd_projection_paired.txt: 134.0 vs 135.8 / 135.7 us at 8 ranks).  Round 4 measured the
+    projection with whole cycles captured: Ld = 5 at 2 and 4 ranks 270.5 / 161.8 vs 287.9 / 170.3 us for Ld = 4,
+    level at 8 ranks (116.9 us both; profiles/r04_dd/dd_projection.txt).  Round 5 makes capture the RCCL default,
+    so the default is now Ld = 5 (the 257^2 level)."""
     from feanet_amd.dd import default_grid
     Pr, Pc = default_grid(P)
-    assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == 4
+    assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == 5
 
 
 def _free_port():

@@ -125,6 +125,36 @@ def test_hjac_vcycle_vs_oracle(T):
             assert err < (1e-10 if T == torch.float64 else 5e-5), (k, err)
 
 
+def test_hjac_vcycle_vs_oracle_full_size():
+    """The MG-HJac cycle exactly as `bench.py --smoother hjac` times it — 4097^2 fp64, L = 12, the shipped HNet
+    weights, the fused schedule (hsweep + restriction, prolongation + hsweep), the fine-level task heights and
+    6-step bodies, staged weight loads, the LDS-resident HJac tail — against the oracle's MultiGrid.Step with every
+    sweep an HRelax (M-FEANet-mg_test.ipynb:147-155, :27346-27372): three cycles from zero, 1e-10 of max|u| after
+    each (~13 s per oracle cycle on the host)."""
+    import os
+    from feanet_amd.solver import MultigridSolver
+    n = 4096
+    w = np.load(os.path.join(os.path.dirname(__file__), "..", "multigrid-feanet_amd", "feanet_amd", "weights",
+                             "hnet_iso_poisson_33x33.npz"))
+    hw = np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+    mg = orc.OracleMultigrid(n, "poisson", np.float64)
+    for l in mg.levels:
+        l.sweep = (lambda ll, o: (lambda v, ff: (lambda j: j + orc.hnet(j - v, ll.geo, hw))(o(v, ff))))(l, l.sweep)
+    rng = np.random.default_rng(4097)
+    f = rng.standard_normal((1, n + 1, n + 1))
+    s = MultigridSolver(n, dtype=torch.float64, smoother="hjac", hnet=hw)
+    assert s.L == 12
+    s.set_rhs(f=torch.from_numpy(f).cuda().reshape(1, 1, n + 1, n + 1))
+    s.load()
+    v = np.zeros_like(f)
+    for k in range(3):
+        s.vcycle()
+        v = mg.step(v, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
+        assert err < 1e-10, (k, err)
+
+
 @pytest.mark.parametrize("T", [torch.float32, torch.float64])
 @pytest.mark.parametrize("problem,n", [("poisson", 1024), ("poisson", 2048), ("interface", 1024)])
 def test_hsweep_vs_oracle_large(T, problem, n):
