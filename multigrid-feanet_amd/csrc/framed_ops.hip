@@ -2291,6 +2291,28 @@ constexpr bool kJoinNTL = FEA_JOIN_NTL != 0;
 #define FEA_JOIN_SHARED 0
 #endif
 constexpr bool kJoinAlternate = FEA_JOIN_ALT != 0;
+// FEA_JOIN_INNER (lab): interior tasks take a join_task instantiation without boundary selects / clamps (measured
+// in the ISA only: the kernel holding both instantiations needs 203-209 VGPRs, two waves per SIMD instead of three).
+// FEA_JOIN_OMZ: a sweep keeps a boundary node's value through a zero omega/d (v = 0 * r + b) instead of a select of
+// the result; the select was compiled as an exec-mask branch per node and stage (fp64 join: 3090 -> 2025 SALU,
+// 428 -> 167 branches in the kernel, 154 -> 145 VGPRs; metric V-cycle 136.8 -> 135.5 us, join 80.0 -> 79.1 us,
+// same-lease A/B twice, profiles/r05_ab/join_omz.txt).  Bitwise: on a boundary node b == the kept value (x = u + w1 P e
+// with every coarse value P reads there on the coarse boundary, i.e. zero), up to the sign of a zero.
+#ifndef FEA_JOIN_INNER
+#define FEA_JOIN_INNER 0
+#endif
+// lab builds (-DFEA_LAB_JREV): every second join launch deals its tasks in reverse order (decode_task_lin's rev) —
+// measured slower (+1.5 us per V-cycle, profiles/r05_ab/join_omz.txt)
+#ifdef FEA_LAB_JREV
+#define FEA_LAB_JOIN_REV(g) { static int flip = 0; (g).rev = flip = !flip; }
+#else
+#define FEA_LAB_JOIN_REV(g)
+#endif
+#ifndef FEA_JOIN_OMZ
+#define FEA_JOIN_OMZ 1
+#endif
+constexpr bool kJoinInner = FEA_JOIN_INNER != 0;
+constexpr bool kJoinOmz = FEA_JOIN_OMZ != 0;
 #define REV_SHARED_LOADS (FEA_JOIN_SHARED != 0)
 
 template <typename T>
@@ -2319,7 +2341,10 @@ struct JoinTask {
   int b, t, I0, I1, c0, cmax;
 };
 
-template <typename T, bool MULTI, bool NT, bool NORM, bool REV, bool NTF>
+// EDGE = false: an interior task (join_interior): every row it streams and every column its lanes load lies inside
+// the grid, so the boundary selects, the row clamps, the lane clamps and the partial stores drop out at compile
+// time (same per-node expressions: bitwise the general task).
+template <typename T, bool MULTI, bool NT, bool NORM, bool REV, bool NTF, bool EDGE = true>
 __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt, const T* tab, const T* rtb,
                                           const T* ptb, double& ssq) {
   constexpr int kJoinAhead = MULTI ? 2 : FEA_JOIN_AHEAD;
@@ -2351,7 +2376,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
   const T w0 = g.w, w1 = g.w2;
   bool cin[V];
 #pragma unroll
-  for (int k = 0; k < V; ++k) cin[k] = cl + k >= 1 && cl + k <= W - 2;
+  for (int k = 0; k < V; ++k) cin[k] = !EDGE || (cl + k >= 1 && cl + k <= W - 2);
   const bool own = lane >= O::L0 && lane < O::L0 + O::OWN;
   const int J0 = (cl + 1) / 2;
   const long long boff = (long long)jt.b * g.bs + F::OFF + cs;
@@ -2367,9 +2392,12 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
   // lanes past the grid's last fine column W - 1 (coarse: Wc - 1) load the last needed lane's columns
   // again instead of streaming columns nothing uses: the last strip of a row can be mostly outside
   // the grid (25 % of the loaded columns at 1025 wide in fp32); stores are masked by column anyway
-  const int ll = min(lane, (W - 1 - cs) / V);
-  const int llc = min(lane, (Wc - 1 - (cs + 1) / 2) / Q);
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+  const int ll = EDGE ? min(lane, (W - 1 - cs) / V) : lane;
+  const int llc = EDGE ? min(lane, (Wc - 1 - (cs + 1) / 2) / Q) : lane;
+  auto rowo = [&](int r) -> long long {
+    if constexpr (EDGE) r = min(max(r, -1), H);
+    return (long long)(r + 1) * ld + V * ll;
+  };
   auto crowo = [&](int a) -> long long { return (long long)(min(max(a, -1), Hc) + 1) * ldc; };
   auto rc = [&](int a) {
     return raw_crow<T, V, MULTI>(eb + crowo(a), MULTI ? pcb + crowo(a) : nullptr, lane, llc);
@@ -2421,14 +2449,21 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
   auto sweep_own = [&](const Row<T, V>& a, const Row<T, V>& b, const Row<T, V>& c, const PRow<V>& pa,
                        const PRow<V>& pb_, const PRow<V>& pc, const T (&fy)[V], const T (&keep)[V], int y,
                        T (&o)[V], bool count) {
-    const bool rin = y >= 1 && y <= H - 2;
+    const bool rin = !EDGE || (y >= 1 && y <= H - 2);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const T acck = kapply<T, V, MULTI>(a, b, c, pa, pb_, pc, k, ks, tab);
       const T omk = MULTI ? tabv(tab, pb_.a[k + 1], 9) : om;
       const T rr = fy[k] - acck;
-      const T v = omk * rr + b.a[k + 1];
-      o[k] = (rin && cin[k]) ? v : keep[k];
+      if constexpr (kJoinOmz) {
+        // boundary nodes: 0 * r + b = b, and b == keep there (the prolonged correction of a boundary node is a
+        // sum of coarse boundary values, all zero, so x = u exactly)
+        const T omz = (rin && cin[k]) ? omk : T(0);
+        o[k] = omz * rr + b.a[k + 1];
+      } else {
+        const T v = omk * rr + b.a[k + 1];
+        o[k] = (rin && cin[k]) ? v : keep[k];
+      }
       if constexpr (NORM)
         if (count && rin && cin[k]) ssq += (double)rr * (double)rr;
     }
@@ -2507,7 +2542,11 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
         const int yw = y - 2 * S;
         const bool ownr = yw >= 2 * I0 - 1 && (yw < 2 * I1 - 1 || I1 == Hc - 1) && yw <= H - 2;
         sweep3(Va, Vb, Vc, P3, P2, P1, f1, keep, yw, w, own && ownr);
-        if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, Ws);
+        if constexpr (EDGE) {
+          if (own && ownr) store_masked<T, V, NT>(ob + rowo(yw), w, cl, Ws);
+        } else {
+          if (own && ownr) vstore<T, V, NT>(ob + rowo(yw), w);
+        }
         Wa = Wb;
         Wb = Wc_;
         Wc_ = own_row<T, V>(w);
@@ -2537,7 +2576,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
           auto put = [&](int I, const T (&o)[Q]) {
             if (own) {
               T* cp = cb + (long long)(I + 1) * ldc;
-              if (J0 + Q - 1 <= Wcs - 2) {
+              if (!EDGE || J0 + Q - 1 <= Wcs - 2) {
                 vstore<T, Q, kCoarseNT && NT>(cp, o);
               } else {
 #pragma unroll
@@ -2668,8 +2707,18 @@ void k_mg_cycle_join(MgArgs<T> g) {
   }
   double ssq = 0.0;
   if (valid) {
-    if (kJoinAlternate && (jt.t & 1)) join_task<T, MULTI, NT, NORM, true, NTF>(g, jt, tab, rtb, ptb, ssq);
-    else join_task<T, MULTI, NT, NORM, false, NTF>(g, jt, tab, rtb, ptb, ssq);
+    // interior task: rows 2 I0 - 4 .. 2 I1 + 2 inside [1, H - 2] (loads reach 2 rows further, still in the frame) and
+    // every loaded column inside [1, W - 2]
+    const int cs = jt.c0 - Ovl3<T>::HL;
+    const bool inner = kJoinInner && g.nrect == 0 && 2 * jt.I0 - 4 >= 1 && 2 * jt.I1 + 2 <= g.H - 2 && cs >= 1 &&
+                       cs + kWave * Frame<T>::VEC - 1 <= g.W - 2;
+    if (kJoinAlternate && (jt.t & 1)) {
+      if (inner) join_task<T, MULTI, NT, NORM, true, NTF, false>(g, jt, tab, rtb, ptb, ssq);
+      else join_task<T, MULTI, NT, NORM, true, NTF, true>(g, jt, tab, rtb, ptb, ssq);
+    } else {
+      if (inner) join_task<T, MULTI, NT, NORM, false, NTF, false>(g, jt, tab, rtb, ptb, ssq);
+      else join_task<T, MULTI, NT, NORM, false, NTF, true>(g, jt, tab, rtb, ptb, ssq);
+    }
   }
   if constexpr (NORM) norm_partial<T>(g, ssq);
 }
@@ -3157,7 +3206,7 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     g.w2 = w1; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc; g.bsc = bsc;                              \
     join_config<T>(B, H, W, g);                                                                              \
     if (g.nt && bs * (long long)sizeof(T) > nt_load_bytes()) g.nt = 2;                                         \
-    if (getenv("FEA_LAB_JREV")) { static int flip = 0; g.rev = flip = !flip; }                                \
+    FEA_LAB_JOIN_REV(g);                                                                                     \
     g.part = norm_ws;                                                                                        \
     const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
     hipStream_t s = (hipStream_t)stream;                                                                     \

@@ -1,4 +1,3 @@
-# (historical record: written for the former FEANET_LIB_OVERRIDE variable; run variant builds through tools/lab/with_lib.py now)
 """Per-workgroup start/end and per-phase times (s_memrealtime, 100 MHz) of the multi-level launches:
 builds the whole library with -DFEA_MID_TRACE into tools/lab/mid_trace.so, runs mid_down / mid_up at
 513^2 (k = 3) and prints the workgroup start/end spread and workgroup 0's phase times.
@@ -14,9 +13,9 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
     from feanet_amd import build
     build.build(out=SO, defines=["FEA_MID_TRACE"])
     sys.exit(0)
-os.environ["FEANET_LIB_OVERRIDE"] = SO
 import torch  # noqa: E402
 from feanet_amd import _lib  # noqa: E402
+_lib.LIB = SO
 from test_gpu_mg import Frame, tables  # noqa: E402
 
 T = torch.float64
