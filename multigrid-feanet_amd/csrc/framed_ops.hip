@@ -717,8 +717,8 @@ __device__ __forceinline__ Row<T, V> own_row(const T (&x)[V]) {  // window L, ow
   Row<T, V> w;
 #pragma unroll
   for (int k = 0; k < V; ++k) w.a[k + 1] = x[k];
-  w.a[0] = shr1(x[V - 1], T(0));
-  w.a[V + 1] = shl1(x[0], T(0));
+  w.a[0] = shr1z(x[V - 1]);
+  w.a[V + 1] = shl1z(x[0]);
   return w;
 }
 template <typename T, int V>
@@ -726,8 +726,8 @@ __device__ __forceinline__ PRow<V> own_prow(const int (&x)[V]) {
   PRow<V> w;
 #pragma unroll
   for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * tab_row_bytes<T>();
-  w.a[0] = shr1(x[V - 1], 0) * tab_row_bytes<T>();
-  w.a[V + 1] = shl1(x[0], 0) * tab_row_bytes<T>();
+  w.a[0] = shr1z(x[V - 1]) * tab_row_bytes<T>();
+  w.a[V + 1] = shl1z(x[0]) * tab_row_bytes<T>();
   return w;
 }
 
@@ -826,7 +826,7 @@ __device__ __forceinline__ void sweep_restrict_task(const MgArgs<T>& g, const Ta
     T r[V + 1];
 #pragma unroll
     for (int k = 0; k < V; ++k) r[k] = sy.f[k] - kapply<T, V, MULTI>(a, b, c, pa.p, sy.p, pc.p, k, ks, tab);
-    r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+    r[V] = shl1z(r[0]);  // column cl+V from the next lane
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       T t;
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
   auto resid = [&](const Wn& a, const Wn& b, const Wn& c, T (&r)[V + 1]) {
 #pragma unroll
     for (int k = 0; k < V; ++k) r[k] = b.f[k] - kapply<T, V, MULTI>(a.v, b.v, c.v, a.p, b.p, c.p, k, ks, tab);
-    r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+    r[V] = shl1z(r[0]);  // column cl+V from the next lane
   };
 
   const int y0 = 2 * I0 - 1;
@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void zr2_task(const MgArgs<T>& g, const TaskId& id, c
     const Wn& c = REV ? x0 : x2;
 #pragma unroll
     for (int k = 0; k < V; ++k) r[k] = x1.f[k] - kapply<T, V, MULTI>(a.v, x1.v, c.v, a.p, x1.p, c.p, k, ks, tab);
-    r[V] = shl1(r[0], T(0));
+    r[V] = shl1z(r[0]);
   };
 
   // ---- stage 2 (level l+1): v' window rows (streaming order, Va oldest); residual rows of f_{l+2}'s row pair
@@ -1762,11 +1762,11 @@ __global__ __launch_bounds__(256) void k_mg_prolong_zu_ovl(MgArgs<T> g) {
     CRow<T, V> c{};
 #pragma unroll
     for (int q = 0; q < Q; ++q) c.e[q + 1] = r.x[q];
-    c.e[0] = shr1(r.x[Q - 1], T(0));
+    c.e[0] = shr1z(r.x[Q - 1]);
     if constexpr (MULTI) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * tab_row_bytes<T>();
-      c.o[0] = shr1(r.p[Q - 1], 0) * tab_row_bytes<T>();
+      c.o[0] = shr1z(r.p[Q - 1]) * tab_row_bytes<T>();
     }
     return c;
   };
@@ -2014,7 +2014,7 @@ __device__ __forceinline__ void prolong2_task(const MgArgs<T>& g, const TaskId& 
     CRow<T, V> c{};
 #pragma unroll
     for (int q = 0; q < Q; ++q) c.e[q + 1] = o[q];
-    c.e[0] = shr1(o[Q - 1], T(0));
+    c.e[0] = shr1z(o[Q - 1]);
     if constexpr (MULTI) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) c.o[q + 1] = b_.p.a[q + 1];
@@ -2558,7 +2558,7 @@ __device__ __forceinline__ void join_task(const MgArgs<T>& g, const JoinTask& jt
             if constexpr (REV) r[k] = f2[k] - kapply<T, V, MULTI>(Wc_, Wb, Wa, P2, P3, P4, k, ks, tab);
             else r[k] = f2[k] - kapply<T, V, MULTI>(Wa, Wb, Wc_, P4, P3, P2, k, ks, tab);
           }
-          r[V] = shl1(r[0], T(0));
+          r[V] = shl1z(r[0]);
           auto term = [&](int q, int ky) -> T {
             T t;
             if constexpr (!MULTI) {

@@ -93,8 +93,8 @@ __device__ __forceinline__ HWin<T, V> hwin(const T (&x)[V]) {
   HWin<T, V> w;
 #pragma unroll
   for (int k = 0; k < V; ++k) w.a[k + 1] = x[k];
-  w.a[0] = shr1(x[V - 1], T(0));
-  w.a[V + 1] = shl1(x[0], T(0));
+  w.a[0] = shr1z(x[V - 1]);
+  w.a[V + 1] = shl1z(x[0]);
   return w;
 }
 
@@ -140,8 +140,8 @@ __device__ __forceinline__ HWin<int, V> hpwin(const int (&x)[V]) {  // pattern o
   HWin<int, V> w;
 #pragma unroll
   for (int k = 0; k < V; ++k) w.a[k + 1] = x[k] * kHTS;
-  w.a[0] = shr1(x[V - 1], 0) * kHTS;
-  w.a[V + 1] = shl1(x[0], 0) * kHTS;
+  w.a[0] = shr1z(x[V - 1]) * kHTS;
+  w.a[V + 1] = shl1z(x[0]) * kHTS;
   return w;
 }
 
@@ -296,11 +296,11 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     CR c{};
 #pragma unroll
     for (int q = 0; q < Q; ++q) c.e[q + 1] = r.x[q];
-    c.e[0] = shr1(r.x[Q - 1], T(0));
+    c.e[0] = shr1z(r.x[Q - 1]);
     if constexpr (MULTI) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) c.o[q + 1] = r.p[q] * kHTS;
-      c.o[0] = shr1(r.p[Q - 1], 0) * kHTS;
+      c.o[0] = shr1z(r.p[Q - 1]) * kHTS;
     }
     return c;
   };
@@ -577,7 +577,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
           }
           r[k] = fr[k] - acc;
         }
-        r[V] = shl1(r[0], T(0));  // column cl+V from the next lane
+        r[V] = shl1z(r[0]);  // column cl+V from the next lane
         stage_t2();
         if constexpr (((ODD ? 1 : 0) + NL) % 2 == 0) {  // row 2I (yr = y - 2 - NL)
 #pragma unroll
