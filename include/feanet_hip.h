@@ -453,26 +453,6 @@ int fea_mg_mid_up_f64(const double* const* f, const double* e, double* out, cons
 /* LDS bytes of one mid launch (up = 0 down, 1 up) with a full TR x TC tile; -1 if it does not fit. */
 long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi);
 
-/* The coarse tail below level a+k (fea_mg_coarse_tail's V(1,1) path, levels Ht x Wt .. with nlev levels, from a zero
- * guess) fused with the k-level prolongation fea_mg_mid_up that consumes its result, in ONE launch: every workgroup of
- * the mid_up grid runs the tail itself and prolongs from the tail's result in LDS (MultiGrid.Step,
- * FEANet/multigrid.py:166-183 / M-FEANet-mg_test.ipynb:27346-27372, from level a+k down and back up to level a).  The
- * level-(a+k) iterate is never written.  f_t, ld_t, bs_t, pid_levels, rtab, w0: the tail's arguments (f_t = level
- * a+k's right-hand side, written by the preceding fea_mg_mid_down; Ht x Wt must be level a+k's size); f, out, pid, k,
- * B, H, W, ktab, omd, ntab, ptab, nptab, w1, TR, TC: fea_mg_mid_up's (without e).  Bitwise fea_mg_coarse_tail followed
- * by fea_mg_mid_up.  For few samples: the tail runs once per workgroup.  FEA_EINVAL if the combined LDS footprint
- * (fea_mg_tail_up_lds_bytes) does not fit. */
-int fea_mg_tail_up_f32(const float* f_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
-                       const uint8_t* pid_levels, const float* rtab, float w0, const float* const* f, float* out,
-                       const uint8_t* const* pid, int k, int B, int H, int W, const float* ktab, const float* omd,
-                       int ntab, const float* ptab, int nptab, float w1, int TR, int TC, void* stream);
-int fea_mg_tail_up_f64(const double* f_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,
-                       const uint8_t* pid_levels, const double* rtab, double w0, const double* const* f, double* out,
-                       const uint8_t* const* pid, int k, int B, int H, int W, const double* ktab, const double* omd,
-                       int ntab, const double* ptab, int nptab, double w1, int TR, int TC, void* stream);
-/* LDS bytes of one fea_mg_tail_up launch; -1 if it does not fit. */
-long long fea_mg_tail_up_lds_bytes(int k, int TR, int TC, int Ht, int Wt, int nlev, int elem_size, int multi);
-
 /* Domain decomposition (feanet_amd.dd): the halo exchange's pack / unpack in one launch.
  * blocks: HOST array of nblocks records {int64 frame (device address of a block in a framed buffer),
  * int64 stage (device address of the block in a staging buffer), int64 ld (row pitch, elements), int32 rows,

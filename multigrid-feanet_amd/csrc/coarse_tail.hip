@@ -11,25 +11,421 @@
 // Semantics = the coarse part of feanet_amd.schedule.vcycle_schedule (every coarse level starts
 // from a zero guess with zero Dirichlet data, FEANet/multigrid.py:171-172; coarsest level gets
 // nu1 + nu2 sweeps; q2 = MM_Interface_error.ipynb's grids[0] pre-smoothing, i.e. none here).
-#ifdef FEA_TAIL_TRACE
-#define FEA_TAIL_TRACE_ON
-#endif
 #include "fea_common.h"
 
-#ifdef FEA_TAIL_TRACE_ON  // lab builds only (tools/lab/tail_lab.py): a timestamp after every barrier
 namespace fea {
-__device__ long long g_tail_trace[256];
-}  // namespace fea
-#define FEA_TAIL_SYNC()                                                                     \
-  do {                                                                                      \
-    __syncthreads();                                                                        \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && nph < 256) fea::g_tail_trace[nph] = clock64(); \
-    ++nph;                                                                                  \
-  } while (0)
-#endif
-#include "tail_core.h"
 
-namespace fea {
+constexpr int kTailThreads = 1024;
+constexpr int kTailMaxLevels = 8;
+constexpr int kTailMaxN = 65;  // per dimension
+constexpr int kTailLdsBytes = 160 * 1024 - 1024;
+constexpr int kTS = 10;  // table stride (9 weights + omega/d)
+
+#ifdef FEA_TAIL_TRACE  // lab builds only (tools/lab/tail_lab.py): a timestamp after every barrier
+__device__ long long g_tail_trace[256];
+#define FEA_TAIL_SYNC()                                                            \
+  do {                                                                             \
+    __syncthreads();                                                               \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && nph < 256) g_tail_trace[nph] = clock64(); \
+    ++nph;                                                                         \
+  } while (0)
+#else
+#define FEA_TAIL_SYNC() __syncthreads()
+#endif
+
+template <typename T>
+struct TailArgs {
+  const T* f_t;
+  T* v_t;
+  const uint8_t* pid;  // compact concatenated per-level maps (NULL: single pattern)
+  const T* ktab;
+  const T* omd;
+  const T* rtab;
+  const T* ptab;
+  T w0, w1;
+  int Ht, Wt, nlev, ld_t;
+  long long bs_t;
+  int ntab, nu1, nu2, q2;
+};
+
+__host__ __device__ inline long long tail_elems(int Ht, int Wt, int nlev) {
+  long long s = 0;
+  for (int k = 0, H = Ht, W = Wt; k < nlev; ++k, H = (H + 1) / 2, W = (W + 1) / 2) s += (long long)H * W;
+  return s;
+}
+
+template <typename T>
+__host__ __device__ inline long long tail_lds_bytes(int Ht, int Wt, int nlev, bool multi) {
+  const long long e = tail_elems(Ht, Wt, nlev);
+  long long b = 3 * e * (long long)sizeof(T);
+  if (multi) b += (e + 15) / 16 * 16;
+  b += 3LL * FEA_MAX_PATTERNS * kTS * sizeof(T);
+  return b;
+}
+
+__device__ __forceinline__ int tail_n(int n0, int k) { return ((n0 - 1) >> k) + 1; }
+__device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element offset of level k in a region
+  int o = 0;
+  for (int j = 0; j < k; ++j) o += tail_n(Ht, j) * tail_n(Wt, j);
+  return o;
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Fused V(1,1) coarse sub-cycle, laid out for latency: ONE workgroup barrier per level and
+// direction, and inside a phase every LDS load of a wave is issued up front (clamped addresses,
+// results masked by selects instead of branches) so the row chains run back to back instead of
+// waiting on one load at a time.  Wave w of the 16 owns a contiguous block of rows of each level,
+// lane c is column c (levels are <= 65 wide; column 64 is a boundary column, read as 0),
+// horizontal neighbours come from DPP row shifts, each row shifted once.  Per level:
+//   down:     v = omd f on the rows the wave's coarse rows need (pointwise, never stored),
+//             r = f - K v, f_c = w0 R r  (level 0 reads f_t straight from HBM)       -> barrier
+//   coarsest: v1 = omd f, v2 = v1 + omd (f - K v1)                                   -> barrier
+//   up:       x = omd f + w1 P e on the rows the wave's sweep reads (the zero-guess pre-smoothed
+//             iterate recomputed, as the streaming kernels do), v' = x + omd (f - K x) -> barrier
+//             (level 0: v' goes straight to HBM)
+// Every node value is the same expression, in the same order, as the general path (bitwise):
+// acc chains start from 0 and add the taps in (row, column) order; x = fma(w1, P e, omd f).
+// ---------------------------------------------------------------------------------------------
+constexpr int kTailDownRows = 2;  // coarse rows per wave going down: Hc - 2 <= 31 over 16 waves
+constexpr int kTailUpRows = 4;    // fine rows per wave going up / at the coarsest level: H - 2 <= 63
+
+// HT != 0: the grid is HT x HT with NLEV levels, known at compile time (every BASELINE configuration
+// ends in the 65^2 .. 3^2 tail), so level sizes, offsets and rows per wave fold into immediates.
+template <typename T, bool MULTI, int HT = 0>
+struct TailFast {
+  const TailArgs<T>& a;
+  T* es;               // per-level corrections (up-sweep outputs), level regions like fs
+  T* fs;               // per-level right-hand sides
+  const T* ktb;        // LDS tables (MULTI)
+  const T* rtb;
+  const T* ptb;
+  const uint8_t* pl;   // LDS pattern maps (MULTI)
+  const T* fg;         // row 0 of this sample's f_t (framed, HBM)
+  T* vg;               // row 0 of this sample's v_t
+  int ld, wv, lane;
+  T kr[9], rr[9], pr[9], om0;
+
+  __device__ __forceinline__ int Hk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Ht, k); }
+  __device__ __forceinline__ int Nk(int k) const { return HT ? ((HT - 1) >> k) + 1 : tail_n(a.Wt, k); }
+
+  // p: byte offset of a pattern's table row (pat(): pattern * kTS * sizeof(T)), so a table read is one
+  // ds_read at p with the tap as its immediate offset
+  __device__ __forceinline__ T tb(const T* t, int p, int d) const {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(t) + p + d * (int)sizeof(T));
+  }
+  __device__ __forceinline__ T omega(int p) const {
+    if constexpr (MULTI) return tb(ktb, p, 9);
+    return om0;
+  }
+  __device__ __forceinline__ T kw(int p, int d) const {
+    if constexpr (MULTI) return tb(ktb, p, d);
+    return kr[d];
+  }
+  __device__ __forceinline__ T rw(int p, int d) const {
+    if constexpr (MULTI) return tb(rtb, p, d);
+    return rr[d];
+  }
+  __device__ __forceinline__ T pw(int p, int d) const {
+    if constexpr (MULTI) return tb(ptb, p, d);
+    return pr[d];
+  }
+  __device__ __forceinline__ bool inside(int H, int N, int y) const {
+    return y >= 1 && y <= H - 2 && lane >= 1 && lane <= N - 2;
+  }
+  // table-row byte offset of node (y, lane)'s pattern (0 off the level), loaded unconditionally
+  __device__ __forceinline__ int pat(const uint8_t* pk, int H, int N, int y) const {
+    if constexpr (MULTI) {
+      const int p = pk[min(max(y, 0), H - 1) * N + min(lane, N - 1)];
+      return (y >= 0 && y < H && lane < N) ? p * (kTS * (int)sizeof(T)) : 0;
+    }
+    return 0;
+  }
+  // (K x) on row j of a register window: rows j-1..j+1 with their DPP-shifted copies
+  template <int R>
+  __device__ __forceinline__ T Kx(int j, const T (&xl)[R], const T (&x)[R], const T (&xr)[R], const int (&ql)[R],
+                                  const int (&q)[R], const int (&qr)[R]) const {
+    T acc = 0;
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      acc += kw(ql[j - 1 + dr], dr * 3 + 0) * xl[j - 1 + dr];
+      acc += kw(q[j - 1 + dr], dr * 3 + 1) * x[j - 1 + dr];
+      acc += kw(qr[j - 1 + dr], dr * 3 + 2) * xr[j - 1 + dr];
+    }
+    return acc;
+  }
+  template <int R>
+  __device__ __forceinline__ void shift(const T (&x)[R], T (&xl)[R], T (&xr)[R]) const {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      xl[j] = shr1z(x[j]);
+      xr[j] = shl1z(x[j]);
+    }
+  }
+  template <int R>
+  __device__ __forceinline__ void shift(const int (&q)[R], int (&ql)[R], int (&qr)[R]) const {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if constexpr (MULTI) {
+        ql[j] = shr1z(q[j]);
+        qr[j] = shl1z(q[j]);
+      } else {
+        ql[j] = qr[j] = 0;
+      }
+    }
+  }
+
+  // level k (offset o) -> f_{k+1}; PER coarse rows per wave.  GLOBAL: f_k is f_t in HBM (level 0);
+  // the wave then also writes the rows it loaded into LDS for the up phase (overlapping rows of
+  // neighbouring waves are written twice with the same value), which replaces a separate staging pass.
+  template <bool GLOBAL, int PER>
+  __device__ __forceinline__ void down_rows(int k, int o, int I0, int I1) const {
+    constexpr int R = 2 * PER + 3;
+    const int H = Hk(k), N = Nk(k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    T* f = fs + o;
+    const uint8_t* pk = pl + o;
+    T* fc = fs + o + H * N;
+    const int yb = 2 * I0 - 2;  // rows yb .. yb + R - 1 (residual rows yb + 1 .. yb + R - 2)
+    T fr[R], v[R], vl[R], vr[R], r[R], rl[R], rrt[R];
+    int q[R], ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int y = min(yb + j, H - 1);
+      if constexpr (GLOBAL) fr[j] = fg[(long long)y * ld + lane];
+      else fr[j] = f[y * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+    if constexpr (GLOBAL) {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (yb + j < H && lane < N) f[(yb + j) * N + lane] = fr[j];
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = inside(H, N, yb + j) ? omega(q[j]) * fr[j] : T(0);
+    shift(v, vl, vr);
+    shift(q, ql, qr);
+    r[0] = r[R - 1] = T(0);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const T kv = keep(Kx(j, vl, v, vr, ql, q, qr));
+      r[j] = inside(H, N, yb + j) ? fr[j] - kv : T(0);
+    }
+    shift(r, rl, rrt);
+    const int J = lane >> 1;
+    const bool st = !(lane & 1) && J >= 1 && J <= Nc - 2;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (I0 + i >= I1) break;
+      T acc = 0;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int j = 2 * i + 1 + ky;
+        acc += rw(ql[j], ky * 3 + 0) * rl[j];
+        acc += rw(q[j], ky * 3 + 1) * r[j];
+        acc += rw(qr[j], ky * 3 + 2) * rrt[j];
+      }
+      acc = keep(acc);
+      if (st) fc[(I0 + i) * Nc + J] = a.w0 * acc;
+    }
+  }
+  template <bool GLOBAL>
+  __device__ __forceinline__ void down(int k, int o) const {
+    constexpr int kWaves = kTailThreads / 64;
+    const int Hc = (Hk(k) + 1) / 2;
+    const int per = (Hc - 2 + kWaves - 1) / kWaves;  // <= kTailDownRows
+    const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
+    if (I0 >= I1) return;  // wave-uniform
+    if (per == 1) down_rows<GLOBAL, 1>(k, o, I0, I1);
+    else down_rows<GLOBAL, kTailDownRows>(k, o, I0, I1);
+  }
+
+  // coarsest level k: v1 = omd f, v2 = v1 + omd (f - K v1); PER rows per wave
+  template <int PER>
+  __device__ __forceinline__ void coarsest_rows(int k, int o, int y0, int y1) const {
+    constexpr int R = PER + 2;
+    const int H = Hk(k), N = Nk(k);
+    const T* f = fs + o;
+    const uint8_t* pk = pl + o;
+    const int yb = y0 - 1;
+    T fr[R], v[R], vl[R], vr[R];
+    int q[R], ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      fr[j] = f[min(yb + j, H - 1) * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = inside(H, N, yb + j) ? omega(q[j]) * fr[j] : T(0);
+    shift(v, vl, vr);
+    shift(q, ql, qr);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const int y = yb + j;
+      if (y >= y1) break;
+      const T kv = Kx(j, vl, v, vr, ql, q, qr);
+      const T w = keep(omega(q[j]) * (fr[j] - kv) + v[j]);
+      if (inside(H, N, y)) {
+        if (k == 0) vg[(long long)y * ld + lane] = w;
+        else es[o + y * N + lane] = w;
+      }
+    }
+  }
+
+  // level k (offset o) from the correction of level k + 1 (offset oc): x = omd f + w1 P e, one sweep.
+  // PAR = parity of the wave's first window row, so every coarse-row index is a compile-time constant;
+  // PER rows per wave.
+  template <int PAR, int PER>
+  __device__ __forceinline__ void up_rows(int k, int o, int oc, int y0, int y1) const {
+    constexpr int R = PER + 2;                // x rows y0-1 .. y0+R-2
+    constexpr int C = (PAR + R) / 2 + 1;      // coarse rows Ib .. Ib+C-1 that they touch
+    const int H = Hk(k), N = Nk(k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
+    const T* f = fs + o;
+    const T* e = es + oc;
+    const uint8_t* pk = pl + o;
+    const uint8_t* pkc = pl + oc;
+    const int yb = y0 - 1, Ib = yb >> 1;  // yb = 2 Ib + PAR
+    const int Ja = (lane + 1) >> 1, Jb = (lane - 1) >> 1;  // even lane: Ja only (kx = 1); odd: Ja (kx = 0), Jb (kx = 2)
+    const bool odd = lane & 1;
+    T fr[R], ea[C], eb[C];
+    int q[R], pa[C], pb[C];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      fr[j] = f[min(yb + j, H - 1) * N + lane];
+      q[j] = pat(pk, H, N, yb + j);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int I = Ib + c, Ic = min(I, Hc - 1);
+      const bool iin = I >= 1 && I <= Hc - 2;
+      const int jA = min(Ja, Nc - 1), jB = max(Jb, 0);
+      const T va = e[Ic * Nc + jA], vb = e[Ic * Nc + jB];
+      ea[c] = (iin && Ja >= 1 && Ja <= Nc - 2) ? va : T(0);
+      eb[c] = (iin && Jb >= 1 && Jb <= Nc - 2) ? vb : T(0);
+      if constexpr (MULTI) {
+        pa[c] = pkc[Ic * Nc + jA] * (kTS * (int)sizeof(T));
+        pb[c] = pkc[Ic * Nc + jB] * (kTS * (int)sizeof(T));
+      } else {
+        pa[c] = pb[c] = 0;
+      }
+    }
+    T x[R], xl[R], xr[R];
+    int ql[R], qr[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      T acc = 0;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        if ((PAR + j + 1 - ky) & 1) continue;  // coarse row (y + 1 - ky) / 2 exists only for even y + 1 - ky
+        const int c = (PAR + j + 1 - ky) >> 1;
+        const T cfa = odd ? pw(pa[c], ky * 3 + 0) : pw(pa[c], ky * 3 + 1);
+        const T t = acc + cfa * ea[c];
+        const T t2 = t + pw(pb[c], ky * 3 + 2) * eb[c];
+        acc = odd ? t2 : t;
+      }
+      const T v0 = omega(q[j]) * fr[j];
+      const T xv = keep(v0 + a.w1 * acc);
+      x[j] = inside(H, N, yb + j) ? xv : T(0);
+    }
+    shift(x, xl, xr);
+    shift(q, ql, qr);
+#pragma unroll
+    for (int j = 1; j < R - 1; ++j) {
+      const int y = yb + j;
+      if (y >= y1) break;
+      const T kx = Kx(j, xl, x, xr, ql, q, qr);
+      const T w = keep(omega(q[j]) * (fr[j] - kx) + x[j]);
+      if (inside(H, N, y)) {
+        if (k == 0) vg[(long long)y * ld + lane] = w;
+        else es[o + y * N + lane] = w;
+      }
+    }
+  }
+
+  // rows 1 .. H-2 of level k over the 16 waves: dispatch on the rows per wave (<= kTailUpRows)
+  template <int PAR>
+  __device__ __forceinline__ void up_par(int k, int o, int oc, int per, int y0, int y1) const {
+    switch (per) {
+      case 1: up_rows<PAR, 1>(k, o, oc, y0, y1); break;
+      case 2: up_rows<PAR, 2>(k, o, oc, y0, y1); break;
+      case 3: up_rows<PAR, 3>(k, o, oc, y0, y1); break;
+      default: up_rows<PAR, kTailUpRows>(k, o, oc, y0, y1); break;
+    }
+  }
+  __device__ __forceinline__ void up(int k, int o, int oc) const {
+    constexpr int kWaves = kTailThreads / 64;
+    const int H = Hk(k);
+    const int per = (H - 2 + kWaves - 1) / kWaves;
+    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+    if (y0 >= y1) return;
+    if ((y0 - 1) & 1) up_par<1>(k, o, oc, per, y0, y1);
+    else up_par<0>(k, o, oc, per, y0, y1);
+  }
+  __device__ __forceinline__ void coarsest(int k, int o) const {
+    constexpr int kWaves = kTailThreads / 64;
+    const int H = Hk(k);
+    const int per = (H - 2 + kWaves - 1) / kWaves;
+    const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+    if (y0 >= y1) return;
+    switch (per) {
+      case 1: coarsest_rows<1>(k, o, y0, y1); break;
+      case 2: coarsest_rows<2>(k, o, y0, y1); break;
+      case 3: coarsest_rows<3>(k, o, y0, y1); break;
+      default: coarsest_rows<kTailUpRows>(k, o, y0, y1); break;
+    }
+  }
+};
+
+template <typename T, bool MULTI, int HT = 0, int NLEV = 0>
+__device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, const T* ktb, const T* rtb,
+                                          const T* ptb, const uint8_t* pl, int wv, int lane
+#ifdef FEA_TAIL_TRACE
+                                          , int& nph
+#endif
+) {
+  const int nlev = NLEV ? NLEV : a.nlev;
+  const long long s0 = (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1) + a.ld_t;
+  TailFast<T, MULTI, HT> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
+  if constexpr (!MULTI) {  // single-pattern tables in registers (uniform loads)
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      t.kr[d] = a.ktab[d];
+      t.rr[d] = a.rtab[d];
+      t.pr[d] = a.ptab[d];
+    }
+    t.om0 = a.omd[0];
+  }
+  // ------------------------------------------------------------------ down
+  // (NLEV != 0: the level loops unroll, so k, the level sizes and offsets are constants in every phase)
+  int o = 0;
+  auto down = [&](int k) {
+    if (k == 0) t.template down<true>(k, o);
+    else t.template down<false>(k, o);
+    o += t.Hk(k) * t.Nk(k);
+    FEA_TAIL_SYNC();
+  };
+  auto up = [&](int k) {
+    const int oc = o;
+    o -= t.Hk(k) * t.Nk(k);
+    t.up(k, o, oc);
+    if (k > 0) FEA_TAIL_SYNC();
+  };
+  if constexpr (NLEV != 0) {
+#pragma unroll
+    for (int k = 0; k + 1 < NLEV; ++k) down(k);
+  } else {
+    for (int k = 0; k + 1 < nlev; ++k) down(k);
+  }
+  // ------------------------------------------------------------------ coarsest: 2 sweeps
+  t.coarsest(nlev - 1, o);
+  if (nlev > 1) FEA_TAIL_SYNC();
+  // ------------------------------------------------------------------ up
+  if constexpr (NLEV != 0) {
+#pragma unroll
+    for (int k = NLEV - 2; k >= 0; --k) up(k);
+  } else {
+    for (int k = nlev - 2; k >= 0; --k) up(k);
+  }
+}
 
 // FIX65: the V(1,1) 65^2 / 6-level tail of every BASELINE configuration only — a kernel of its own, so the
 // register allocation is that path's alone (sharing one kernel with the general paths spilled 16 VGPRs of
@@ -41,7 +437,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
   __shared__ __attribute__((aligned(16))) char smem[kTailLdsBytes];
   const int tid = threadIdx.x;
   const int nlev = a.nlev, Ht = a.Ht, Wt = a.Wt;
-#ifdef FEA_TAIL_TRACE_ON
+#ifdef FEA_TAIL_TRACE
   int nph = 0;
   if (tid == 0 && blockIdx.x == 0) g_tail_trace[255] = clock64();
 #endif
@@ -96,16 +492,16 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     // the first down phase reads f_t from HBM itself and stages it for the up phase; single pattern:
     // the tables come from uniform loads, so nothing has to land before it
     if (MULTI) FEA_TAIL_SYNC();
-    tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane, TailOut<T>{(int)blockIdx.x}
-#ifdef FEA_TAIL_TRACE_ON
+    tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+#ifdef FEA_TAIL_TRACE
                                , nph
 #endif
     );
     return;
   } else if (fast) {
     if (MULTI || nlev == 1) FEA_TAIL_SYNC();
-    tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane, TailOut<T>{(int)blockIdx.x}
-#ifdef FEA_TAIL_TRACE_ON
+    tail_fast<T, MULTI>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
+#ifdef FEA_TAIL_TRACE
                         , nph
 #endif
     );
@@ -284,7 +680,7 @@ static inline bool tail_dim_ok(int n, int nlev) {
 FEA_TAIL_API(f32, float)
 FEA_TAIL_API(f64, double)
 
-#ifdef FEA_TAIL_TRACE_ON
+#ifdef FEA_TAIL_TRACE
 extern "C" int fea_tail_trace_read(long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tail_trace), sizeof(long long) * 256, 0, hipMemcpyDeviceToHost);
 }

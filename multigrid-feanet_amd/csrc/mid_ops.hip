@@ -26,7 +26,6 @@
 // uint8 pattern maps per level) are supported; the regions are read in the framed layout of
 // fea_mg_layout at every level.
 #include "fea_common.h"
-#include "tail_core.h"
 
 namespace fea {
 
@@ -115,7 +114,6 @@ struct StageJob {
   E* dst;
   Reg g;
   int H, W, ld, off;
-  int dp = 0;    // row pitch of dst (0: the region's width)
 };
 template <typename E, int N>
 __device__ __forceinline__ void stage_batch(const StageJob<E> (&jobs)[N]) {
@@ -144,11 +142,10 @@ __device__ __forceinline__ void stage_batch(const StageJob<E> (&jobs)[N]) {
       const StageJob<E>& J = jobs[q];
       const int c = J.g.c0 + lane;
       const bool cok = c >= 0 && c < J.W;
-      const int dp = J.dp ? J.dp : J.g.nc;
 #pragma unroll
       for (int i = 0; i < kStageRows; ++i) {
         const int yy = base + wv + i * NW, y = J.g.r0 + yy;
-        if (yy < J.g.nr && lane < J.g.nc) J.dst[yy * dp + lane] = (cok && y >= 0 && y < J.H) ? v[q][i] : E(0);
+        if (yy < J.g.nr && lane < J.g.nc) J.dst[yy * J.g.nc + lane] = (cok && y >= 0 && y < J.H) ? v[q][i] : E(0);
       }
     }
     if (!more) break;
@@ -428,28 +425,13 @@ struct MidUpGeo {
   int fx[kMidMaxK], uo[kMidMaxK + 1], po[kMidMaxK + 1], ko;
 };
 
-// LDS bytes of the fused kernel's tail part (TailFast's fast path: iterates and right-hand sides of every tail level,
-// two-material tables and pattern maps), rounded to 16
-__host__ __device__ inline long long tail_up_tail_bytes(int Ht, int Wt, int nlev, int esz, bool multi) {
-  const long long tot = tail_elems(Ht, Wt, nlev);
-  long long b = 2 * tot * esz;
-  if (multi) b += 3LL * FEA_MAX_PATTERNS * kTS * esz + (tot + 15) / 16 * 16;
-  return (b + 15) / 16 * 16;
-}
-
-// TAIL != 0 (fea_mg_tail_up): the workgroup first runs the whole coarse tail below level a+k itself (tail_core.h,
-// TailFast's V(1,1) path; 2 = the 65^2 / 6-level instantiation), every workgroup redundantly, with the tail's result
-// going to the LDS region U[k] its prolongation reads — the tail's own launch, its write of level a+k's iterate and
-// this kernel's staging of it disappear, and the staging of f_a .. f_{a+k-1} shares one memory round trip with the
-// tail's f_t.  For one or a few samples only (the tail is latency-bound: a copy per workgroup costs nothing then).
-template <typename T, bool MULTI, int K, int TAIL = 0>
-__global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a, TailArgs<T> ta) {
+template <typename T, bool MULTI, int K>
+__global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kMidLdsBytes];
   __shared__ MidUpGeo geo;
   FEA_MID_MARK(2 * blockIdx.x);
   constexpr int OFF = 128 / (int)sizeof(T) - 1;
   constexpr int k = K;
-  constexpr bool TL = TAIL != 0;
   const int tiles = a.ntr * a.ntc;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int b = bid / tiles, t = bid - b * tiles, ti = t / a.ntc, tj = t - ti * a.ntc;
@@ -462,19 +444,10 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a, TailArg
     for (int j = 0; j < k; ++j) u[j + 1] = mid_coarse_of(u[j]);
   }
   auto xreg = [&](int j) { return Reg{u[j].r0 - 1, u[j].c0 - 1, u[j].nr + 2, u[j].nc + 2}; };
-  // tail part (TAIL): es, fs of every tail level, two-material tables and maps, at the start of LDS
-  const int ttot = TL ? (int)tail_elems(ta.Ht, ta.Wt, ta.nlev) : 0;
-  T* const tes = reinterpret_cast<T*>(smem);
-  T* const tfs = tes + ttot;
-  T* const tktb = tfs + ttot;
-  T* const trtb = tktb + (MULTI ? FEA_MAX_PATTERNS * kTS : 0);
-  T* const tptb = trtb + (MULTI ? FEA_MAX_PATTERNS * kTS : 0);
-  uint8_t* const tpl = reinterpret_cast<uint8_t*>(tptb + (MULTI ? FEA_MAX_PATTERNS * kTS : 0));
-  char* const mid0 = smem + (TL ? tail_up_tail_bytes(ta.Ht, ta.Wt, ta.nlev, (int)sizeof(T), MULTI) : 0);
   // LDS carve: Fx[j] (f on x region j), U[j+1], X scratch, tables, patterns
   T* Fx[kMidMaxK];
   T* U[kMidMaxK + 1];
-  T* p = reinterpret_cast<T*>(mid0);
+  T* p = reinterpret_cast<T*>(smem);
   int xmax = 0;
 #pragma unroll
   for (int j = 0; j < k; ++j) {
@@ -502,17 +475,10 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a, TailArg
   const TabLoad<T> tl = tables_issue<T>(a.ktab, a.omd, a.xtab, a.ntab, a.nx);
   // stage everything up front (one round of memory latency for the whole launch)
   {
-    StageJob<T> jf[k + 1 + TL];
+    StageJob<T> jf[k + 1];
 #pragma unroll
     for (int j = 0; j < k; ++j) jf[j] = {a.f[j] + (long long)b * a.bs[j], Fx[j], xreg(j), a.H[j], a.W[j], a.ld[j], OFF};
-    if constexpr (TL) {
-      // the tail's top right-hand side, whole, into its fs (row pitch Wt <= 65: 64 columns, then column 64)
-      const T* src = ta.f_t + (long long)b * ta.bs_t;
-      jf[k] = {src, tfs, Reg{0, 0, ta.Ht, min(ta.Wt, 64)}, ta.Ht, ta.Wt, ta.ld_t, OFF, ta.Wt};
-      jf[k + 1] = {src, tfs + 64, Reg{0, 64, ta.Ht, max(ta.Wt - 64, 0)}, ta.Ht, ta.Wt, ta.ld_t, OFF, ta.Wt};
-    } else {
-      jf[k] = {a.e + (long long)b * a.bs[k], U[k], u[k], a.H[k], a.W[k], a.ld[k], OFF};
-    }
+    jf[k] = {a.e + (long long)b * a.bs[k], U[k], u[k], a.H[k], a.W[k], a.ld[k], OFF};
     if constexpr (MULTI) {
       StageJob<uint8_t> jp[k + 1];
 #pragma unroll
@@ -520,21 +486,8 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a, TailArg
       stage_batch<uint8_t, k + 1>(jp);
     }
     FEA_MID_WAVE_MARK(0);
-    stage_batch<T, k + 1 + TL>(jf);
+    stage_batch<T, k + 1>(jf);
     FEA_MID_WAVE_MARK(1);
-  }
-  if constexpr (TL) {
-    // the sink region starts at zero: the tail writes its interior nodes only (boundary / outside stay 0, as in HBM)
-    for (int i = threadIdx.x; i < u[k].nr * u[k].nc; i += kMidThreads) U[k][i] = T(0);
-    if constexpr (MULTI) {
-      for (int i = threadIdx.x; i < ta.ntab * kTS; i += kMidThreads) {
-        const int pp = i / kTS, d = i - pp * kTS;
-        tktb[i] = d == 9 ? ta.omd[pp] : ta.ktab[pp * 9 + d];
-        trtb[i] = d == 9 ? T(0) : ta.rtab[pp * 9 + d];
-        tptb[i] = d == 9 ? T(0) : ta.ptab[pp * 9 + d];
-      }
-      for (int i = threadIdx.x; i < ttot; i += kMidThreads) tpl[i] = ta.pid[i];
-    }
   }
   tables_commit<T>(tl, ktb0, xtb0, a.ntab, a.nx);
   if (MULTI && threadIdx.x == 0) {
@@ -548,13 +501,6 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_up(MidArgs<T> a, TailArg
     geo.ko = (int)(ktb0 - reinterpret_cast<T*>(smem));
   }
   FEA_MID_SYNC(0);
-  if constexpr (TL) {
-    const TailOut<T> to{b, U[k], u[k].r0, u[k].c0, u[k].nr, u[k].nc};
-    const int twv = threadIdx.x >> 6, tlane = threadIdx.x & 63;
-    if constexpr (TAIL == 2) tail_fast<T, MULTI, 65, 6, true, true>(ta, tes, tfs, tktb, trtb, tptb, tpl, twv, tlane, to);
-    else tail_fast<T, MULTI, 0, 0, true, true>(ta, tes, tfs, tktb, trtb, tptb, tpl, twv, tlane, to);
-    FEA_MID_SYNC(0);  // U[k] complete
-  }
   T ks[9], ps[9], om = T(0);
   if constexpr (!MULTI) {
 #pragma unroll
@@ -774,23 +720,6 @@ static void mid_launch(Kern k1, Kern k2, Kern k3, Kern k4, int k, dim3 grid, voi
   Kern kern = k == 1 ? k1 : k == 2 ? k2 : k == 3 ? k3 : k4;
   hipLaunchKernelGGL(kern, grid, dim3(kMidThreads), 0, (hipStream_t)stream, a);
 }
-template <typename T, bool MULTI, typename Kern>
-static void mid_launch(Kern k1, Kern k2, Kern k3, Kern k4, int k, dim3 grid, void* stream, const MidArgs<T>& a,
-                       const TailArgs<T>& ta) {
-  Kern kern = k == 1 ? k1 : k == 2 ? k2 : k == 3 ? k3 : k4;
-  hipLaunchKernelGGL(kern, grid, dim3(kMidThreads), 0, (hipStream_t)stream, a, ta);
-}
-
-// (n - 1) divisible by 2^(nlev-1) and every level >= 3 nodes (as the coarse tail's host check)
-static inline bool tail_up_dim_ok(int n, int nlev) {
-  if (n < 3 || n > kTailMaxN) return false;
-  for (int j = 1; j < nlev; ++j) {
-    if ((n - 1) & 1) return false;
-    n = (n + 1) / 2;
-    if (n < 3) return false;
-  }
-  return true;
-}
 
 #define FEA_MID_API(SUF, T)                                                                                      \
   extern "C" int fea_mg_mid_down_##SUF(const T* const* f, const uint8_t* const* pid, int k, int B, int H, int W, \
@@ -838,53 +767,10 @@ static inline bool tail_up_dim_ok(int n, int nlev) {
     a.ntr = (a.H[0] - 2 + TR - 1) / TR;                                                                          \
     a.ntc = (a.W[0] - 2 + TC - 1) / TC;                                                                          \
     const dim3 grid(B * a.ntr * a.ntc);                                                                          \
-    const TailArgs<T> ta = {};                                                                                   \
     if (multi) mid_launch<T, true>(k_mg_mid_up<T, true, 1>, k_mg_mid_up<T, true, 2>, k_mg_mid_up<T, true, 3>,     \
-                                   k_mg_mid_up<T, true, 4>, k, grid, stream, a, ta);                              \
+                                   k_mg_mid_up<T, true, 4>, k, grid, stream, a);                                  \
     else mid_launch<T, false>(k_mg_mid_up<T, false, 1>, k_mg_mid_up<T, false, 2>, k_mg_mid_up<T, false, 3>,      \
-                              k_mg_mid_up<T, false, 4>, k, grid, stream, a, ta);                                  \
-    FEA_LAUNCH_CHECK();                                                                                          \
-  }                                                                                                              \
-  extern "C" int fea_mg_tail_up_##SUF(const T* f_t, int Ht, int Wt, int nlev, int ld_t, long long bs_t,          \
-                                      const uint8_t* pid_levels, const T* rtab, T w0, const T* const* f, T* out,  \
-                                      const uint8_t* const* pid, int k, int B, int H, int W, const T* ktab,       \
-                                      const T* omd, int ntab, const T* ptab, int nptab, T w1, int TR, int TC,     \
-                                      void* stream) {                                                            \
-    MidArgs<T> a = {};                                                                                           \
-    if (!f_t || !rtab || !f || !out || !ktab || !omd || !ptab || ntab < 1 || ntab > FEA_MAX_PATTERNS)          \
-      return FEA_EINVAL;                                                                                         \
-    const bool multi = ntab > 1;                                                                                 \
-    if ((multi && (!pid || !pid_levels || nptab != ntab)) || (!multi && nptab != 1)) return FEA_EINVAL;         \
-    if (mid_fill<T>(a, k, B, H, W, TR, TC)) return FEA_EINVAL;                                                   \
-    if (nlev < 1 || nlev > kTailMaxLevels || Ht != a.H[k] || Wt != a.W[k] || !tail_up_dim_ok(Ht, nlev) ||       \
-        !tail_up_dim_ok(Wt, nlev) || ld_t != a.ld[k] || bs_t != a.bs[k])                                        \
-      return FEA_EINVAL;                                                                                         \
-    if (mid_up_lds(k, TR, TC, (int)sizeof(T), multi) + tail_up_tail_bytes(Ht, Wt, nlev, (int)sizeof(T), multi) > \
-        kMidLdsBytes)                                                                                            \
-      return FEA_EINVAL;                                                                                         \
-    for (int j = 0; j <= k; ++j) {                                                                               \
-      if ((j < k && (!f[j] || f[j] == out)) || (multi && !pid[j])) return FEA_EINVAL;                           \
-      a.f[j] = j < k ? f[j] : nullptr;                                                                           \
-      a.pid[j] = multi ? pid[j] : nullptr;                                                                       \
-    }                                                                                                            \
-    a.e = nullptr; a.out = out;                                                                                  \
-    a.ktab = ktab; a.omd = omd; a.xtab = ptab; a.w = w1; a.ntab = ntab; a.nx = nptab;                           \
-    a.ntr = (a.H[0] - 2 + TR - 1) / TR;                                                                          \
-    a.ntc = (a.W[0] - 2 + TC - 1) / TC;                                                                          \
-    TailArgs<T> ta{f_t, nullptr, multi ? pid_levels : nullptr, ktab, omd, rtab, ptab, w0, w1, Ht, Wt, nlev, ld_t,  \
-                   bs_t, ntab, 1, 1, 0};                                                                        \
-    const dim3 grid(B * a.ntr * a.ntc);                                                                          \
-    const bool fix65 = Ht == 65 && Wt == 65 && nlev == 6;                                                        \
-    if (multi && fix65) mid_launch<T, true>(k_mg_mid_up<T, true, 1, 2>, k_mg_mid_up<T, true, 2, 2>,              \
-                                            k_mg_mid_up<T, true, 3, 2>, k_mg_mid_up<T, true, 4, 2>, k, grid, stream, \
-                                            a, ta);                                                             \
-    else if (multi) mid_launch<T, true>(k_mg_mid_up<T, true, 1, 1>, k_mg_mid_up<T, true, 2, 1>,                  \
-                                        k_mg_mid_up<T, true, 3, 1>, k_mg_mid_up<T, true, 4, 1>, k, grid, stream, a, ta); \
-    else if (fix65) mid_launch<T, false>(k_mg_mid_up<T, false, 1, 2>, k_mg_mid_up<T, false, 2, 2>,              \
-                                         k_mg_mid_up<T, false, 3, 2>, k_mg_mid_up<T, false, 4, 2>, k, grid, stream, \
-                                         a, ta);                                                                \
-    else mid_launch<T, false>(k_mg_mid_up<T, false, 1, 1>, k_mg_mid_up<T, false, 2, 1>, k_mg_mid_up<T, false, 3, 1>, \
-                              k_mg_mid_up<T, false, 4, 1>, k, grid, stream, a, ta);                               \
+                              k_mg_mid_up<T, false, 4>, k, grid, stream, a);                                      \
     FEA_LAUNCH_CHECK();                                                                                          \
   }
 
@@ -896,15 +782,6 @@ extern "C" int fea_mid_trace_read(long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mid_trace), sizeof(long long) * 4096, 0, hipMemcpyDeviceToHost);
 }
 #endif
-
-extern "C" long long fea_mg_tail_up_lds_bytes(int k, int TR, int TC, int Ht, int Wt, int nlev, int elem_size,
-                                             int multi) {
-  if (k < 1 || k > kMidMaxK || TR < 1 || TC < 1 || (elem_size != 4 && elem_size != 8) || nlev < 1 ||
-      nlev > kTailMaxLevels || !tail_up_dim_ok(Ht, nlev) || !tail_up_dim_ok(Wt, nlev))
-    return -1;
-  const long long b = mid_up_lds(k, TR, TC, elem_size, multi != 0) + tail_up_tail_bytes(Ht, Wt, nlev, elem_size, multi != 0);
-  return b <= kMidLdsBytes ? b : -1;
-}
 
 extern "C" long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi) {
   if (k < 1 || k > kMidMaxK || TR < 1 || TC < 1 || (elem_size != 4 && elem_size != 8)) return -1;

@@ -22,9 +22,6 @@ Steps:
   ("mid_up", a, k, csrc, dst, T)       the "omdf" prolong_sweep steps of levels a+k-1..a in one
                                        launch: u_a[dst] from u_{a+k}[csrc] (tile T of level a)
                                        (group_mid rewrites a schedule into these)
-  ("tail_up", t, a, k, dst, T)         ("coarse_tail", t, x) followed by ("mid_up", a, k, x, dst, T) with
-                                       a + k = t, in one launch (every workgroup of the mid_up grid runs
-                                       the tail; fuse_tail_up rewrites a schedule into these)
 
 Semantics reproduced:
   * nu1 = nu2 = 1: MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372) == MultiGrid.iterate
@@ -318,26 +315,6 @@ def group_mid(steps, pick_down, pick_up):
                     m += 1
             i = j + 1
             continue
-        out.append(st)
-        i += 1
-    return out
-
-
-def fuse_tail_up(steps, can_fuse):
-    """Rewrite ("coarse_tail", t, x) directly followed by the ("mid_up", a, k, x, dst, T) that prolongs from its
-    result (a + k = t) into ("tail_up", t, a, k, dst, T) where can_fuse(t, a, k, T) allows it."""
-    out = []
-    i = 0
-    while i < len(steps):
-        st = steps[i]
-        if (st[0] == "coarse_tail" and i + 1 < len(steps) and steps[i + 1][0] == "mid_up"):
-            mu = steps[i + 1]
-            t, x = st[1], st[2]
-            a, k, csrc, dst, T = mu[1:6]
-            if a + k == t and csrc == x and can_fuse(t, a, k, T):
-                out.append(("tail_up", t, a, k, dst, T))
-                i += 2
-                continue
         out.append(st)
         i += 1
     return out

@@ -25,18 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-
-_CUS = {}
-
-
-def _num_cus(device):
-    """Compute units of the device (cached)."""
-    i = torch.device(device).index or 0
-    if i not in _CUS:
-        _CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
-    return _CUS[i]
-from .schedule import (OMDF, fuse_tail_up, group_mid, hjac_schedule, pair_prolongations, pair_restrictions,
-                       vcycle_schedule)
+from .schedule import OMDF, group_mid, hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
 
 
 _SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
@@ -133,9 +122,6 @@ class MultigridSolver:
             (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels).
         pair_levels: two consecutive zero-guess restrictions, and two recomputed-iterate prolongations, left
             to single-level launches run as one each (fea_mg_zero_restrict2 / fea_mg_prolong2, bitwise the two).
-        tail_up: the coarse tail and the multi-level prolongation that consumes its result run as one launch
-            (fea_mg_tail_up: every workgroup runs the tail itself; bitwise the two launches) where each workgroup
-            gets a CU of its own (single samples).
     """
 
     MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
@@ -146,7 +132,7 @@ class MultigridSolver:
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_levels=True, tail_up=True):
+                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_levels=True):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -180,7 +166,6 @@ class MultigridSolver:
         self.join_cycles = join_cycles
         self.mid = bool(mid)
         self.pair_levels = bool(pair_levels)
-        self.tail_up = bool(tail_up)
         if smoother not in ("jac", "hjac"):
             raise ValueError(f"MultigridSolver: unknown smoother {smoother!r}")
         self.smoother = smoother
@@ -434,24 +419,7 @@ class MultigridSolver:
             if self.pair_levels:
                 ok = lambda l: l + 2 < self.L and self.levels[l + 2].H >= 3 and self.levels[l + 2].W >= 3
                 steps = pair_prolongations(pair_restrictions(steps, ok), ok)
-            if self.tail_up:
-                steps = fuse_tail_up(steps, self._can_tail_up)
         return [self.bind_step(st) for st in steps], end
-
-    def _can_tail_up(self, t, a, k, T):
-        """The coarse tail from level t fused into the mid_up launch of levels t-1 .. a (fea_mg_tail_up): V(1,1)
-        schedules (the tail's fast path), every workgroup of that launch on a CU of its own (each runs the whole
-        tail: the tail is latency-bound, so copies on otherwise idle CUs cost nothing, but a second round of
-        workgroups would double it), and the combined LDS footprint fits."""
-        if self.nu1 != 1 or self.nu2 != 1 or self.compat is not None:
-            return False
-        TR, TC = T if isinstance(T, tuple) else (T, T)
-        la, lt = self.levels[a], self.levels[t]
-        tiles = self.B * -(-(la.H - 2) // TR) * -(-(la.W - 2) // TC)
-        if tiles > _num_cus(self.device):
-            return False
-        esz = 4 if self.dtype == torch.float32 else 8
-        return _lib.tail_up_lds_bytes(k, TR, TC, lt.H, lt.W, self.L - t, esz, self.ntab > 1) > 0
 
     def _mid_tile(self, up, a, k):
         """Tile size for a multi-level launch over levels a..a+k-1 (down: tile of level a+k; up: of
@@ -554,15 +522,6 @@ class MultigridSolver:
             TR, TC = T if isinstance(T, tuple) else (T, T)
             return ("mg_mid_up", (fs, ptr(a + k, csrc), ptr(a, dst), pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt,
                                   pt, npt, self.w[1], TR, TC))
-        if kind == "tail_up":
-            t, a, k, dst, T = st[1:6]
-            fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + k)])
-            pids = _lib.PtrArray([pid(j) for j in range(a, a + k + 1)]) if nt > 1 else None
-            TR, TC = T if isinstance(T, tuple) else (T, T)
-            return ("mg_tail_up", (lv[t].f.data_ptr(), lv[t].H, lv[t].W, self.L - t, lv[t].ld, lv[t].bs,
-                                   None if self.tail_pid is None else self.tail_pid.data_ptr(), rt, self.w[0], fs,
-                                   ptr(a, dst), pids, k, self.B, lv[a].H, lv[a].W, kt, om, nt, pt, npt, self.w[1], TR,
-                                   TC))
         if kind == "coarse_tail":
             t = l
             return ("mg_coarse_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
@@ -1048,19 +1007,16 @@ class MultigridSolver:
                 else:  # read u, f, e; write out
                     total += nodes * (3 * esz + pb) + coarse * (esz + pb)
                 continue
-            if name in ("mg_mid_down", "mg_mid_up", "mg_tail_up"):
-                k, B, H, W = (args[4:8] if name == "mg_mid_up" else args[12:16] if name == "mg_tail_up" else
-                              args[2:6])
+            if name in ("mg_mid_down", "mg_mid_up"):
+                k, B, H, W = args[4:8] if name == "mg_mid_up" else args[2:6]
                 sizes = []
                 for _ in range(k + 1):
                     sizes.append(B * (H - 2) * (W - 2))
                     H, W = (H + 1) // 2, (W + 1) // 2
                 if name == "mg_mid_down":  # read f_a, write f_{a+1..a+k}
                     total += esz * sum(sizes) + pb * sum(sizes[:-1])
-                elif name == "mg_mid_up":  # read f_a..f_{a+k-1}, u_{a+k}; write u_a
+                else:  # read f_a..f_{a+k-1}, u_{a+k}; write u_a
                     total += esz * (sum(sizes) + sizes[0]) + pb * sum(sizes)
-                else:  # read f_a..f_{a+k-1}; write u_a (u_{a+k} comes from the tail in LDS; the tail as coarse_tail)
-                    total += esz * (sum(sizes[:-1]) + sizes[0]) + pb * sum(sizes)
                 continue
             if name == "mg_zero_restrict2":  # read f_l (+ pattern), write f_{l+1}, f_{l+2}
                 B, H, W = args[-9:-6]

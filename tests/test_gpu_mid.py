@@ -1,4 +1,4 @@
-"""GPU parity of the multi-level launches (fea_mg_mid_down / fea_mg_mid_up / fea_mg_tail_up, mid_ops.hip).
+"""GPU parity of the multi-level launches (fea_mg_mid_down / fea_mg_mid_up, mid_ops.hip).
 
 They must equal the per-level kernels they replace BITWISE (same per-node expressions, same order):
 mid_down against a chain of fea_mg_residual_restrict(u = NULL, v_out = NULL), mid_up against a chain
@@ -130,7 +130,7 @@ def test_solver_mid_bitwise(problem, n, B, T):
     for mid in (True, False):
         s = MultigridSolver(n, problem=problem, dtype=T, batch=B, mid=mid)
         kinds = [c[0] for c in s._plan("a")[0]]
-        assert ("mg_mid_down" in kinds) == mid and ("mg_mid_up" in kinds or "mg_tail_up" in kinds) == mid, kinds
+        assert ("mg_mid_down" in kinds) == mid and ("mg_mid_up" in kinds) == mid, kinds
         s.set_rhs(f=f)
         s.load()
         s.vcycle()
@@ -152,91 +152,3 @@ def test_solver_rect_mid_bitwise():
         s.vcycle(2)
         outs.append(s.solution())
     assert torch.equal(outs[0], outs[1])
-
-
-TAIL_CASES = [  # (intervals at level a, k, up tile, tail levels from level a+k down)
-    (512, 3, 32, 6),  # the metric cycle's 513^2 -> 65^2 prolongation after the 65^2 .. 3^2 tail (65^2 / 6-level form)
-    (512, 3, 32, 2),  # C2's 65 -> 33 tail
-    (256, 2, 16, 6), (128, 2, 8, 5), (64, 1, 5, 3),
-]
-
-
-@pytest.mark.parametrize("T", [torch.float32, torch.float64])
-@pytest.mark.parametrize("problem,learned", [("poisson", False), ("interface", True)])
-@pytest.mark.parametrize("n,k,tile,nlev", TAIL_CASES)
-@pytest.mark.parametrize("B", [1, 2])
-def test_tail_up_bitwise(T, problem, learned, n, k, tile, nlev, B):
-    """fea_mg_tail_up (every workgroup runs the coarse tail, then prolongs from its result in LDS) == fea_mg_coarse_tail
-    followed by fea_mg_mid_up, bitwise, boundary of u_a untouched."""
-    from feanet_amd import _lib, mesh_setup as ms
-    rng = np.random.default_rng(7 * n + k + nlev + B)
-    npdt = np.float32 if T == torch.float32 else np.float64
-    ktab, omd, R, P, kt, om, rt, pt = tables(problem, T, learned)
-    nt = ktab.shape[0]
-    w0, w1 = 0.9, 0.75
-    lv = chain(n, n, k, B, T, problem)
-    for j in range(k + 1):
-        f = rng.standard_normal((B, lv[j].H, lv[j].W)).astype(npdt)
-        f[:, 0, :] = f[:, -1, :] = f[:, :, 0] = f[:, :, -1] = 0
-        lv[j].put("f", f)
-    Nt = lv[k].H
-    pidl = None
-    if problem == "interface":
-        maps = [ms.interface_pattern_map(((Nt - 1) >> j) + 1).reshape(-1) for j in range(nlev)]
-        pidl = torch.from_numpy(np.concatenate(maps)).cuda()
-    pl = None if pidl is None else pidl.data_ptr()
-    fs = _lib.PtrArray([x.L.f.data_ptr() for x in lv[:k]])
-    H, W = lv[0].H, lv[0].W
-    _lib.call("mg_coarse_tail", T, lv[k].L.f.data_ptr(), lv[k].L.a.data_ptr(), Nt, Nt, nlev, lv[k].L.ld, lv[k].L.bs, pl,
-              kt.data_ptr(), om.data_ptr(), nt, rt.data_ptr(), pt.data_ptr(), w0, w1, 1, 1, 0, B, None)
-    lv[0].put("b", np.full((B, H, W), 9.0, npdt))
-    _lib.call("mg_mid_up", T, fs, lv[k].L.a.data_ptr(), lv[0].L.b.data_ptr(), pid_arr(lv, problem), k, B, H, W,
-              kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(), nt, w1, tile, tile, None)
-    ref = lv[0].get("b").copy()
-    lv[0].put("b", np.full((B, H, W), 9.0, npdt))
-    assert _lib.tail_up_lds_bytes(k, tile, tile, Nt, Nt, nlev, np.dtype(npdt).itemsize, problem == "interface") > 0
-    _lib.call("mg_tail_up", T, lv[k].L.f.data_ptr(), Nt, Nt, nlev, lv[k].L.ld, lv[k].L.bs, pl, rt.data_ptr(), w0, fs,
-              lv[0].L.b.data_ptr(), pid_arr(lv, problem), k, B, H, W, kt.data_ptr(), om.data_ptr(), nt, pt.data_ptr(),
-              nt, w1, tile, tile, None)
-    out = lv[0].get("b")
-    assert np.array_equal(out, ref), f"tail_up differs: max {np.abs(out - ref).max():.3e}"
-
-
-def test_tail_up_rejects_mismatched_levels():
-    """The tail's top level must be level a+k of the prolongation (size, framed layout)."""
-    from feanet_amd import _lib
-    lv = chain(256, 256, 2, 1, torch.float64, "poisson")
-    ktab, omd, R, P, kt, om, rt, pt = tables("poisson", torch.float64)
-    fs = _lib.PtrArray([x.L.f.data_ptr() for x in lv[:2]])
-    with pytest.raises(RuntimeError, match="invalid arguments"):  # 33^2 is not level a+2 = 65^2
-        _lib.call("mg_tail_up", torch.float64, lv[2].L.f.data_ptr(), 33, 33, 5, lv[2].L.ld, lv[2].L.bs, None,
-                  rt.data_ptr(), 1.0, fs, lv[0].L.b.data_ptr(), None, 2, 1, lv[0].H, lv[0].W, kt.data_ptr(),
-                  om.data_ptr(), 1, pt.data_ptr(), 1, 1.0, 16, 16, None)
-
-
-@pytest.mark.parametrize("problem,n,B,T,fused", [("poisson", 4096, 1, torch.float64, True),
-                                                  ("poisson", 1024, 1, torch.float64, True),
-                                                  ("interface", 2048, 1, torch.float64, True),
-                                                  ("poisson", 1024, 1, torch.float32, True),
-                                                  ("poisson", 1024, 3, torch.float32, False)])
-def test_solver_tail_up_bitwise(problem, n, B, T, fused):
-    """MultigridSolver with the tail fused into the prolongation launch == without (bitwise), single and joined
-    cycles; batches whose prolongation grid exceeds the CUs keep the two launches."""
-    from feanet_amd.solver import MultigridSolver
-    g = torch.Generator(device="cuda")
-    g.manual_seed(5)
-    f = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=T, generator=g)
-    outs = []
-    for tu in (True, False):
-        s = MultigridSolver(n, problem=problem, dtype=T, batch=B, tail_up=tu)
-        kinds = [c[0] for c in s._plan("a")[0]]
-        assert ("mg_tail_up" in kinds) == (tu and fused), kinds
-        assert ("mg_coarse_tail" in kinds) != (tu and fused), kinds
-        s.set_rhs(f=f)
-        s.load()
-        s.vcycle()
-        one = s.solution()
-        s.vcycle(3)
-        outs.append((one, s.solution(), s.residual_norm()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    assert torch.equal(outs[0][2], outs[1][2])

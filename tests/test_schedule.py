@@ -365,17 +365,3 @@ def test_vcycle_blocks_cover_k(k):
     assert sum(b != G for b in pb) <= 1 and (pb[-1] == k % G if k % G else pb[-1] == G)
     gb = MultigridSolver.graph_blocks(k, G)
     assert sum(gb) == k and all(b & (b - 1) == 0 for b in gb)
-
-
-def test_fuse_tail_up():
-    """A coarse tail followed by the multi-level prolongation of its result becomes one ("tail_up") step; a tail whose
-    result another step reads, a prolongation from another buffer, or a refused fusion stay two steps."""
-    from feanet_amd.schedule import fuse_tail_up
-    steps = [("mid_down", 3, 3, 4), ("coarse_tail", 6, "a"), ("mid_up", 3, 3, "a", "b", 32), ("prolong_sweep2", 1)]
-    assert fuse_tail_up(steps, lambda *a: True) == [("mid_down", 3, 3, 4), ("tail_up", 6, 3, 3, "b", 32),
-                                                    ("prolong_sweep2", 1)]
-    assert fuse_tail_up(steps, lambda *a: False) == steps
-    other = [("coarse_tail", 6, "a"), ("mid_up", 3, 3, "b", "b", 32)]
-    assert fuse_tail_up(other, lambda *a: True) == other
-    gap = [("coarse_tail", 6, "a"), ("mid_up", 2, 3, "a", "b", 32)]  # a + k != t
-    assert fuse_tail_up(gap, lambda *a: True) == gap
