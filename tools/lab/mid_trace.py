@@ -42,7 +42,7 @@ for name, call in (("down", lambda: _lib.call("mg_mid_down", T, fs, None, k, 1, 
     st = [buf[2 * i] for i in range(nwg)]
     en = [buf[2 * i + 1] for i in range(nwg)]
     t0 = min(st)
-    ph = [buf[2048 + i] for i in range(2 * k + 1)]
+    ph = [buf[2048 + i] for i in range(9)]
     print(f"{name}: WG start spread {(max(st) - t0) * 10} ns, first end {(min(en) - t0) * 10} ns, "
           f"last end {(max(en) - t0) * 10} ns; WG0 phases (ns from its start): "
           + " ".join(str((p - st[0]) * 10) for p in ph), flush=True)

@@ -35,12 +35,13 @@ Ht = int(os.environ.get("HT", 65))
 nl = int(os.environ.get("NLEV", 6))
 ld = ((Ht + 16 + 15) // 16) * 16
 bs = (Ht + 2) * ld
-f = torch.randn(bs, dtype=T, device=dev)
-v = torch.zeros(bs, dtype=T, device=dev)
+B = int(os.environ.get("B", 1))  # B samples = B workgroups, one per CU (B = 256: every CU runs a tail at once)
+f = torch.randn(B * bs, dtype=T, device=dev)
+v = torch.zeros(B * bs, dtype=T, device=dev)
 buf = (ctypes.c_longlong * 256)()
 for rep in range(3):
     rc = L.fea_mg_coarse_tail_f64(f.data_ptr(), v.data_ptr(), Ht, Ht, nl, ld, bs, None, ktab.data_ptr(),
-                                  omd.data_ptr(), 1, rtab.data_ptr(), rtab.data_ptr(), 1.0, 1.0, 1, 1, 0, 1, s)
+                                  omd.data_ptr(), 1, rtab.data_ptr(), rtab.data_ptr(), 1.0, 1.0, 1, 1, 0, B, s)
     assert rc == 0, rc
     torch.cuda.synchronize()
 L.fea_tail_trace_read(buf)
@@ -52,5 +53,5 @@ for i in range(255):
         break
     out.append(buf[i] - prev)
     prev = buf[i]
-print(f"Ht={Ht} nlev={nl}: total {prev - t0} cycles over {len(out)} phases")
+print(f"B={B} Ht={Ht} nlev={nl}: total {prev - t0} cycles over {len(out)} phases")
 print(" ".join(str(x) for x in out))
