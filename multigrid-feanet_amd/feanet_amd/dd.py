@@ -51,12 +51,16 @@ def global_levels(m, n):
     return L
 
 
-def default_agglomeration(m, n, P, L, max_nodes=1 << 18, Pc=1):
+def default_agglomeration(m, n, P, L, max_nodes=None, Pc=1):
     """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows (P row
-    blocks, Pc column blocks).  2^18: at 8193^2 (BASELINE C4) the 257^2 level, Ld = 5 — with whole cycles
-    captured (the RCCL default) the per-rank projection is fastest there at 2 and 4 ranks and ties Ld = 4 at 8
-    (270.5 / 161.8 / 116.9 us vs 287.9 / 170.3 / 116.9, profiles/r04_dd/dd_projection.txt): the replicated
-    coarse sub-cycle is shorter, the wider ghost frames cost less than that."""
+    blocks, Pc column blocks).  Default max_nodes: 2^18 below 8 ranks, 2^20 from 8 on — at 8193^2 (BASELINE C4)
+    Ld = 5 (257^2) at 2 and 4 ranks, Ld = 4 (513^2) at 8: the per-rank projection with whole cycles captured (the
+    RCCL default) runs 267.0 / 160.7 us at Ld = 5 vs 285.6 / 167.5 at Ld = 4 on 2 / 4 ranks (the replicated coarse
+    sub-cycle is shorter, the doubled ghost frames of the small levels cost less), and 116.7 at Ld = 4 vs 119.2 at
+    Ld = 5 on 8, where the blocks are small enough that the doubled ghost frames cost more
+    (profiles/r05_dd/dd_projection.txt)."""
+    if max_nodes is None:
+        max_nodes = (1 << 20) if P * Pc >= 8 else (1 << 18)
     Ld = 1
     while Ld < L - 1 and ((m >> Ld) + 1) * ((n >> Ld) + 1) > max_nodes and m % (P << (Ld + 1)) == 0 \
             and m // (P << (Ld + 1)) >= 4 and n % (Pc << (Ld + 1)) == 0 and (Pc == 1 or n // (Pc << (Ld + 1)) >= 4):
