@@ -453,6 +453,34 @@ int fea_mg_mid_up_f64(const double* const* f, const double* e, double* out, cons
 /* LDS bytes of one mid launch (up = 0 down, 1 up) with a full TR x TC tile; -1 if it does not fit. */
 long long fea_mg_mid_lds_bytes(int up, int k, int TR, int TC, int elem_size, int multi);
 
+/* Two consecutive coarse levels a, a+1 of the learned-smoother V(1,1) cycle in ONE launch each way (hmid_ops.hip;
+ * tiles with recomputed halos, every stage an LDS pass; bitwise the streaming kernels they replace).  Levels a,
+ * a+1, a+2 are framed buffers (fea_mg_layout) of H x W, (H+1)/2 x (W+1)/2, ...; pid[0..2] their pattern maps
+ * (NULL array when ntab == 1); hw = nlayers 3x3 HNet weights.
+ * hmid_down: the zero-guess HRelax pre-sweep + residual + restriction of levels a and a+1 (two
+ *   fea_mg_hsweep_restrict(u = NULL) calls, M-FEANet-mg_test.ipynb MultiGrid.Step :27346-27360 with
+ *   Relax = HJacIterator.HRelax :147-155): reads f[0] = f_a, writes u[0] = u_a, f[1] = f_(a+1), u[1] = u_(a+1),
+ *   f[2] = f_(a+2) (interior).  Tile T x T of level a+2.
+ * hmid_up: the prolongation + correction + HRelax post-sweep of levels a+1 and a from e = u_(a+2) (two
+ *   fea_mg_prolong_hsweep calls, :27362-27372): reads f[0..1] = f_a, f_(a+1), u[0..1] = the stored iterates
+ *   u_a, u_(a+1); writes out = the new u_a (interior); the new u_(a+1) is not stored.  Tile T x T of level a.
+ * Both return FEA_EINVAL if the tile's LDS footprint (fea_mg_hmid_lds_bytes) does not fit. */
+int fea_mg_hmid_down_f32(const float* const* f, float* const* u, const uint8_t* const* pid, int B, int H, int W,
+                         const float* ktab, const float* omd, int ntab, const float* hw, int nlayers,
+                         const float* rtab, int nrtab, float w0, int T, void* stream);
+int fea_mg_hmid_down_f64(const double* const* f, double* const* u, const uint8_t* const* pid, int B, int H, int W,
+                         const double* ktab, const double* omd, int ntab, const double* hw, int nlayers,
+                         const double* rtab, int nrtab, double w0, int T, void* stream);
+int fea_mg_hmid_up_f32(const float* const* f, const float* const* u, const float* e, float* out,
+                       const uint8_t* const* pid, int B, int H, int W, const float* ktab, const float* omd, int ntab,
+                       const float* hw, int nlayers, const float* ptab, int nptab, float w1, int T, void* stream);
+int fea_mg_hmid_up_f64(const double* const* f, const double* const* u, const double* e, double* out,
+                       const uint8_t* const* pid, int B, int H, int W, const double* ktab, const double* omd,
+                       int ntab, const double* hw, int nlayers, const double* ptab, int nptab, double w1, int T,
+                       void* stream);
+/* LDS bytes of one hmid launch (up = 0 down, 1 up) with a full T x T tile; -1 if it does not fit. */
+long long fea_mg_hmid_lds_bytes(int up, int T, int nlayers, int elem_size, int multi);
+
 /* Domain decomposition (feanet_amd.dd): the halo exchange's pack / unpack in one launch.
  * blocks: HOST array of nblocks records {int64 frame (device address of a block in a framed buffer),
  * int64 stage (device address of the block in a staging buffer), int64 ld (row pitch, elements), int32 rows,

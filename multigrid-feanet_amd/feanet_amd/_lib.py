@@ -60,6 +60,8 @@ _SIGS = {
     # several coarse levels per launch (pointer arrays: ptr_array())
     "mg_mid_down": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
     "mg_mid_up": [P, P, P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
+    "mg_hmid_down": [P, P, P, I, I, I, P, P, I, P, I, P, I, "S", I, P],
+    "mg_hmid_up": [P, P, P, P, P, I, I, I, P, P, I, P, I, P, I, "S", I, P],
 }
 _EXTRA = {
     "fea_abi_version": ([], I),
@@ -70,6 +72,7 @@ _EXTRA = {
     "fea_mg_coarse_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
     "fea_mg_hjac_tail_lds_bytes": ([I, I, I, I, I], ctypes.c_size_t),
     "fea_mg_mid_lds_bytes": ([I, I, I, I, I, I], LL),
+    "fea_mg_hmid_lds_bytes": ([I, I, I, I, I], LL),
     "fea_interface_pattern_map": ([P, LL, I, I, F64, P], I),
     "fea_dd_copy_blocks": ([P, I, I, I, P], I),
     "fea_dd_copy_rects": ([P, I, I, P], I),
@@ -175,6 +178,10 @@ def stencil_grad_ws_bytes(ntab, B, H, W):
 
 def mid_lds_bytes(up, k, TR, TC, elem_size, multi):
     return int(lib().fea_mg_mid_lds_bytes(int(bool(up)), k, TR, TC, elem_size, int(bool(multi))))
+
+
+def hmid_lds_bytes(up, T, nlayers, elem_size, multi):
+    return int(lib().fea_mg_hmid_lds_bytes(int(bool(up)), T, nlayers, elem_size, int(bool(multi))))
 
 
 class PtrArray:

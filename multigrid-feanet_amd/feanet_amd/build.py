@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(HERE, "libfeanet_hip.so")
 SOURCES = ["generic_ops.hip", "framed_ops.hip", "coarse_tail.hip", "hnet_ops.hip", "mid_ops.hip", "setup_ops.hip",
-           "dd_ops.hip", "hjac_tail.hip"]
+           "dd_ops.hip", "hjac_tail.hip", "hmid_ops.hip"]
 ARCH = os.environ.get("FEANET_ARCH", "gfx950")
 
 

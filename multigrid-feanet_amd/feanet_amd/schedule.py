@@ -199,6 +199,34 @@ def hjac_schedule(L, nu1=1, nu2=1, start="a", tail_from=None, fuse=False):
     return steps, cur[0]
 
 
+def group_hmid(steps, pairs):
+    """Rewrite the fused HJac V(1,1) steps (hjac_schedule(fuse=True)) of two consecutive coarse levels a, a+1 into
+    one launch each way, for every (a, T_down, T_up) in `pairs`: the two zero-guess
+    ("hsweep_restrict", a, None, da), ("hsweep_restrict", a+1, None, da1) become ("hmid_down", a, da, da1, T_down)
+    (fea_mg_hmid_down), and ("prolong_hsweep", a+1, u1, e, d1), ("prolong_hsweep", a, u0, d1, d0) become
+    ("hmid_up", a, u0, u1, e, d0, T_up) (fea_mg_hmid_up; level a+1's new iterate is not stored) — bitwise the
+    pairs.  Steps that do not have that shape (nu1, nu2 != 1, a stored guess) are left alone."""
+    want = {a: (td, tu) for a, td, tu in pairs}
+    out = []
+    i = 0
+    while i < len(steps):
+        st = steps[i]
+        nx = steps[i + 1] if i + 1 < len(steps) else None
+        if (nx is not None and st[0] == "hsweep_restrict" and nx[0] == "hsweep_restrict" and st[1] in want
+                and nx[1] == st[1] + 1 and st[2] is None and nx[2] is None):
+            out.append(("hmid_down", st[1], st[3], nx[3], want[st[1]][0]))
+            i += 2
+            continue
+        if (nx is not None and st[0] == "prolong_hsweep" and nx[0] == "prolong_hsweep" and nx[1] in want
+                and st[1] == nx[1] + 1 and nx[3] == st[4]):
+            out.append(("hmid_up", nx[1], nx[2], st[2], st[3], nx[4], want[nx[1]][1]))
+            i += 2
+            continue
+        out.append(st)
+        i += 1
+    return out
+
+
 def pair_restrictions(steps, can_pair):
     """Rewrite two consecutive single-level zero-guess restrictions (("resid_restrict", l, None, None), then
     the same at l + 1) into one ("resid_restrict2", l) step — fea_mg_zero_restrict2, bitwise the two —

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import OMDF, group_mid, hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
+from .schedule import OMDF, group_hmid, group_mid, hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
 
 
 _SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
@@ -119,7 +119,8 @@ class MultigridSolver:
             pre-smooth + residual + restriction of the next as one pass (fea_mg_cycle_join; bitwise
             the same result, 28 instead of 52 B per node between two cycles).  V(1,1) Jacobi only.
         mid: run latency-bound coarse levels (B*H*W <= MID_NODES) up to four per launch
-            (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels).
+            (fea_mg_mid_down / fea_mg_mid_up, bitwise the per-level kernels); with smoother="hjac", two per
+            launch (fea_mg_hmid_down / fea_mg_hmid_up, bitwise the fused per-level HJac kernels).
         pair_levels: two consecutive zero-guess restrictions, and two recomputed-iterate prolongations, left
             to single-level launches run as one each (fea_mg_zero_restrict2 / fea_mg_prolong2, bitwise the two).
     """
@@ -128,6 +129,7 @@ class MultigridSolver:
     #                       streaming kernels win: tools/lab/mid_lab.py)
     MID_MIN_TILES = 200   # workgroups a multi-level launch should give the 256 CUs
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
+    HMID_MIN_TILES = 64   # workgroups an HJac two-level launch should give the CUs (one per CU: LDS)
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
@@ -411,6 +413,8 @@ class MultigridSolver:
         if self.smoother == "hjac":
             steps, end = hjac_schedule(self.L, self.nu1, self.nu2, start, tail_from=self.hjac_tail_from,
                                        fuse=self.fuse)
+            if self.mid and self.fuse:
+                steps = group_hmid(steps, self._pick_hmid())
         else:
             steps, end = vcycle_schedule(self.L, self.nu1, self.nu2, self.compat, start, self.tail_from, self.fuse,
                                          top_zero=self.zero_start)
@@ -443,6 +447,37 @@ class MultigridSolver:
             if tiles >= self.MID_MIN_TILES:
                 return T
         return best
+
+    def _hmid_tile(self, up, a):
+        """Tile size of an HJac two-level launch over levels a, a+1 (down: tile of level a+2; up: of level a):
+        the largest whose LDS footprint fits and that gives >= HMID_MIN_TILES workgroups, else the smallest that
+        fits (None: none does)."""
+        esz = 4 if self.dtype == torch.float32 else 8
+        tl = self.levels[a if up else a + 2]
+        fit = [T for T in ((64, 32, 16, 8) if up else (16, 8, 4, 2))
+               if _lib.hmid_lds_bytes(up, T, self.nl, esz, self.ntab > 1) > 0]
+        for T in fit:
+            if self.B * -(-(tl.H - 2) // T) * -(-(tl.W - 2) // T) >= self.HMID_MIN_TILES:
+                return T
+        return fit[-1] if fit else None
+
+    def _pick_hmid(self):
+        """(a, T_down, T_up) for the HJac levels paired into two-level launches: streamed coarse levels (a >= 1,
+        above the HJac tail) of <= MID_NODES nodes, paired from the coarse end upward."""
+        top = self.hjac_tail_from if self.hjac_tail_from is not None else self.L - 1
+        el = [l for l in range(1, top) if self.B * self.levels[l].H * self.levels[l].W <= self.MID_NODES]
+        pairs = []
+        hi = len(el)
+        while hi >= 2:
+            a = el[hi - 2]
+            if el[hi - 1] == a + 1 and a + 2 < self.L:
+                td, tu = self._hmid_tile(False, a), self._hmid_tile(True, a)
+                if td and tu:
+                    pairs.append((a, td, tu))
+                    hi -= 2
+                    continue
+            hi -= 1
+        return pairs
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
@@ -536,6 +571,20 @@ class MultigridSolver:
             return ("mg_prolong_hsweep", (ptr(l, st[2]), None, ptr(l + 1, st[3]), f, ptr(l, st[4]), pid(l), pid(l + 1), kt,
                                           om, nt, self.hw.data_ptr(), self.nl, pt, npt, self.w[1]) + geom(l) +
                     cgeom(l))
+        if kind == "hmid_down":
+            a, da, da1, T = st[1:5]
+            fs = _lib.PtrArray([lv[j].f.data_ptr() for j in range(a, a + 3)])
+            us = _lib.PtrArray([ptr(a, da), ptr(a + 1, da1)])
+            pids = _lib.PtrArray([pid(j) for j in range(a, a + 3)]) if nt > 1 else None
+            return ("mg_hmid_down", (fs, us, pids, self.B, lv[a].H, lv[a].W, kt, om, nt, self.hw.data_ptr(), self.nl,
+                                     rt, nr, self.w[0], T))
+        if kind == "hmid_up":
+            a, u0, u1, esrc, dst, T = st[1:7]
+            fs = _lib.PtrArray([lv[a].f.data_ptr(), lv[a + 1].f.data_ptr()])
+            us = _lib.PtrArray([ptr(a, u0), ptr(a + 1, u1)])
+            pids = _lib.PtrArray([pid(j) for j in range(a, a + 3)]) if nt > 1 else None
+            return ("mg_hmid_up", (fs, us, ptr(a + 2, esrc), ptr(a, dst), pids, self.B, lv[a].H, lv[a].W, kt, om, nt,
+                                   self.hw.data_ptr(), self.nl, pt, npt, self.w[1], T))
         if kind == "hjac_tail":
             t = l
             return ("mg_hjac_tail", (lv[t].f.data_ptr(), ptr(t, st[2]), lv[t].H, lv[t].W, self.L - t, lv[t].ld,
@@ -1006,6 +1055,17 @@ class MultigridSolver:
                     total += nodes * (esz * (3 if args[0] is not None else 2) + pb) + coarse * esz
                 else:  # read u, f, e; write out
                     total += nodes * (3 * esz + pb) + coarse * (esz + pb)
+                continue
+            if name in ("mg_hmid_down", "mg_hmid_up"):
+                B, H, W = args[3:6] if name == "mg_hmid_down" else args[5:8]
+                n = []
+                for _ in range(3):
+                    n.append(B * (H - 2) * (W - 2))
+                    H, W = (H + 1) // 2, (W + 1) // 2
+                if name == "mg_hmid_down":  # read f_a; write u_a, f_(a+1), u_(a+1), f_(a+2)
+                    total += esz * (2 * n[0] + 2 * n[1] + n[2]) + pb * (n[0] + n[1])
+                else:  # read u_a, f_a, u_(a+1), f_(a+1), e; write u_a
+                    total += esz * (3 * n[0] + 2 * n[1] + n[2]) + pb * (n[0] + n[1] + n[2])
                 continue
             if name in ("mg_mid_down", "mg_mid_up"):
                 k, B, H, W = args[4:8] if name == "mg_mid_up" else args[2:6]

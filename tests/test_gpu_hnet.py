@@ -346,3 +346,67 @@ def test_hjac_fused_schedule_bitwise(T, problem, n, B, nu):
         out.append(sols)
     for k, (a, b) in enumerate(zip(*out)):
         assert torch.equal(a, b), (k, (a - b).abs().max().item())
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,m,n,B,nl,nu", [("poisson", 512, 512, 1, 3, (1, 1)), ("poisson", 1024, 1024, 2, 3, (1, 1)),
+                                                 ("poisson", 256, 512, 1, 2, (1, 1)), ("poisson", 512, 512, 1, 1, (2, 1)),
+                                                 ("poisson", 512, 512, 2, 3, (1, 2)), ("interface", 512, 512, 1, 3, (1, 1)),
+                                                 ("interface", 512, 512, 2, 2, (1, 1))])
+@pytest.mark.parametrize("tiles", ["default", "largest", "smallest"])
+def test_hjac_hmid_bitwise(T, problem, m, n, B, nl, nu, tiles):
+    """fea_mg_hmid_down / fea_mg_hmid_up (two HJac levels per launch, hmid_ops.hip) are bitwise the fused per-level
+    kernels they replace (mid=False): whole V-cycles, both problems, batches, 1-3 HNet layers, rows != columns,
+    V(2,1) / V(1,2) (only the up / down pairs apply), every tile size the solver may pick."""
+    from feanet_amd.solver import MultigridSolver
+    rng = np.random.default_rng(m + n + B + nl)
+    hw = (0.25 * rng.standard_normal((nl, 3, 3))).astype(np.float32)
+    f = torch.from_numpy(rng.standard_normal((B, 1, m + 1, n + 1))).to("cuda", T)
+    kw = dict(dtype=T, batch=B, smoother="hjac", hnet=hw, problem=problem, nu1=nu[0], nu2=nu[1],
+              rows=None if m == n else m)
+    out = []
+    for mid in (True, False):
+        s = MultigridSolver(n, mid=mid, **kw)
+        if tiles != "default":
+            s.HMID_MIN_TILES = 1 if tiles == "largest" else 1 << 30
+        kinds = [name for name, _ in s._plan("a")[0]]
+        assert (kinds.count("mg_hmid_down") > 0) == (mid and nu[0] == 1), kinds
+        assert (kinds.count("mg_hmid_up") > 0) == (mid and nu[1] == 1), kinds
+        s.set_rhs(f=f)
+        s.load()
+        sols = []
+        for _ in range(3):
+            s.vcycle()
+            sols.append(s.solution())
+        out.append(sols)
+    for k, (a, b) in enumerate(zip(*out)):
+        assert torch.equal(a, b), (k, (a - b).abs().max().item())
+
+
+def test_hmid_api_rejects_bad_arguments():
+    """fea_mg_hmid_down / _up return FEA_EINVAL (RuntimeError) for even level sizes, a tile whose LDS does not
+    fit, missing pattern maps with per-pattern tables, and an output aliasing an input."""
+    from feanet_amd import _lib
+    from feanet_amd.solver import _Level
+    T = torch.float64
+    lv = [_Level(256 >> j, 256 >> j, 1, T, torch.device("cuda")) for j in range(3)]
+    kt = torch.ones(9, device="cuda", dtype=T)
+    om = torch.ones(1, device="cuda", dtype=T)
+    hw = torch.zeros(27, device="cuda", dtype=T)
+    fs = _lib.PtrArray([l.f.data_ptr() for l in lv])
+    us = _lib.PtrArray([lv[0].a.data_ptr(), lv[1].a.data_ptr()])
+    ok = (fs, us, None, 1, 257, 257, kt.data_ptr(), om.data_ptr(), 1, hw.data_ptr(), 3, kt.data_ptr(), 1, 1.0)
+    assert _lib.hmid_lds_bytes(False, 8, 3, 8, False) > 0 and _lib.hmid_lds_bytes(False, 64, 3, 8, False) == -1
+    assert _lib.hmid_lds_bytes(True, 32, 3, 8, False) > 0 and _lib.hmid_lds_bytes(True, 128, 3, 8, False) == -1
+    for bad in (dict(H=256), dict(TT=64), dict(ntab=16, nr=16)):
+        args = list(ok) + [bad.get("TT", 8), None]
+        if "H" in bad:
+            args[4] = bad["H"]
+        if "ntab" in bad:
+            args[8], args[12] = bad["ntab"], bad["nr"]
+        with pytest.raises(RuntimeError, match="invalid arguments"):
+            _lib.call("mg_hmid_down", T, *args)
+    with pytest.raises(RuntimeError, match="invalid arguments"):
+        _lib.call("mg_hmid_up", T, _lib.PtrArray([lv[0].f.data_ptr(), lv[1].f.data_ptr()]), us, lv[2].a.data_ptr(),
+                  lv[0].a.data_ptr(), None, 1, 257, 257, kt.data_ptr(), om.data_ptr(), 1, hw.data_ptr(), 3,
+                  kt.data_ptr(), 1, 1.0, 16, None)

@@ -38,6 +38,11 @@ def interpret(mg, steps, v, f, compat=None):
             expanded += [("resid_restrict", st[1], None, None), ("resid_restrict", st[1] + 1, None, None)]
         elif st[0] == "prolong_sweep2":  # feanet_amd.schedule.pair_prolongations
             expanded += [("prolong_sweep", st[1] + 1, "omdf", st[2], "mid"), ("prolong_sweep", st[1], "omdf", "mid", st[3])]
+        elif st[0] == "hmid_down":  # feanet_amd.schedule.group_hmid
+            expanded += [("hsweep_restrict", st[1], None, st[2]), ("hsweep_restrict", st[1] + 1, None, st[3])]
+        elif st[0] == "hmid_up":
+            a, u0, u1, e, d0 = st[1:6]
+            expanded += [("prolong_hsweep", a + 1, u1, e, "mid"), ("prolong_hsweep", a, u0, "mid", d0)]
         else:
             expanded.append(st)
     for st in expanded:
@@ -166,6 +171,30 @@ def test_hjac_tail_schedule_equals_step(problem, tail, fuse):
                 lvl.sweep = (lambda ll, o: (lambda x, ff: (lambda j: j + orc.hnet(j - x, ll.geo, mg.hw))(o(x, ff))))(
                     lvl, lvl.sweep)
             np.testing.assert_allclose(out, mg.step(v, f), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("nu", [(1, 1), (2, 1), (1, 2)])
+@pytest.mark.parametrize("pairs", [[(1, 8, 32)], [(2, 8, 32)], [(1, 4, 16), (3, 4, 16)]])
+def test_hmid_grouping_equals_per_level(problem, nu, pairs):
+    """group_hmid (two HJac levels per launch each way, fea_mg_hmid_down / _up) is the fused per-level schedule:
+    the down pair only where both levels start from the zero guess (nu1 = 1), the up pair wherever two
+    prolongation + sweep steps follow each other (nu2 = 1)."""
+    from feanet_amd.schedule import group_hmid, hjac_schedule
+    n, L = 64, 6
+    rng = np.random.default_rng(17)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    mg.nu, mg.hw = nu, 0.3 * rng.standard_normal((3, 3, 3))
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    ref_steps, end = hjac_schedule(L, *nu, tail_from=5, fuse=True)
+    steps = group_hmid(ref_steps, pairs)
+    kinds = [st[0] for st in steps]
+    assert kinds.count("hmid_down") == (len(pairs) if nu[0] == 1 else 0), steps
+    assert kinds.count("hmid_up") == (len(pairs) if nu[1] == 1 else 0), steps
+    out = interpret(mg, steps, v, f)[0][end]
+    ref = interpret(mg, ref_steps, v, f)[0][end]
+    np.testing.assert_array_equal(out, ref)
 
 
 @pytest.mark.parametrize("problem", ["poisson", "interface"])

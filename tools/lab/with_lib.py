@@ -13,6 +13,11 @@ from feanet_amd import _lib  # noqa: E402
 
 if sys.argv[1] != "-":
     _lib.LIB = os.path.abspath(sys.argv[1])
+    _hmid = _lib.hmid_lds_bytes
+
+    def _hmid_or_none(*a):  # builds older than the HJac two-level launches: none fits
+        return _hmid(*a) if hasattr(_lib.lib(), "fea_mg_hmid_lds_bytes") else -1
+    _lib.hmid_lds_bytes = _hmid_or_none
 sys.argv = sys.argv[2:]
 sys.path.insert(0, os.path.dirname(os.path.abspath(sys.argv[0])))
 runpy.run_path(sys.argv[0], run_name="__main__")
