@@ -2,7 +2,7 @@
 #   bash tools/gpu_check.sh TAG
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}; export TMPDIR=/tmp; T=gpurun_out/$1; mkdir -p $T
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $T/pytest.log 2>&1 || { tail -30 $T/pytest.log; exit 1; }
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $T/pytest.log 2>&1 || { tail -30 $T/pytest.log; exit 1; }
 tail -2 $T/pytest.log
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.log 2>&1 || { tail $T/smoke.log; exit 1; }
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $T/bench.json 2> $T/bench.err || { tail $T/bench.err; exit 1; }
