@@ -410,3 +410,77 @@ def test_hmid_api_rejects_bad_arguments():
         _lib.call("mg_hmid_up", T, _lib.PtrArray([lv[0].f.data_ptr(), lv[1].f.data_ptr()]), us, lv[2].a.data_ptr(),
                   lv[0].a.data_ptr(), None, 1, 257, 257, kt.data_ptr(), om.data_ptr(), 1, hw.data_ptr(), 3,
                   kt.data_ptr(), 1, 1.0, 16, None)
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("problem,m,n,B", [("poisson", 256, 256, 2), ("poisson", 128, 512, 1), ("interface", 256, 256, 1)])
+@pytest.mark.parametrize("nl", [0, 1, 2, 3])
+def test_hmid_kernels_vs_per_level_calls(T, problem, m, n, B, nl):
+    """The C-ABI of the HJac two-level launches against the per-level calls they replace, every HNet depth the ABI
+    takes (0-3 layers), per-pattern R/P, rectangles, batches, every tile size that fits: fea_mg_hmid_down is bitwise
+    fea_mg_hsweep_restrict(u = NULL) on levels a and a+1 (iterates, both coarse right-hand sides), fea_mg_hmid_up
+    bitwise fea_mg_prolong_hsweep on levels a+1 then a; boundary nodes of every output untouched."""
+    from feanet_amd import _lib, mesh_setup as ms
+    from feanet_amd.solver import _Level
+    if problem == "interface" and m != n:
+        pytest.skip("two-material problem is square")
+    rng = np.random.default_rng(m + n + B + nl)
+    dev = torch.device("cuda")
+    pids = [ms.interface_pattern_map((m >> j) + 1) if problem == "interface" else None for j in range(3)]
+    lv = [_Level(m >> j, n >> j, B, T, dev, pids[j]) for j in range(3)]
+    kt, om, nt, rt, pt = _tables(problem, T, rng)
+    hw = torch.from_numpy((0.25 * rng.standard_normal((max(nl, 1), 3, 3))).astype(np.float32).reshape(-1)).cuda().to(T)
+    put = lambda L, name, x: L.view(L.buf(name)).copy_(torch.from_numpy(x).to(T))
+    get = lambda L, name: L.view(L.buf(name)).clone()
+    pid = lambda j: None if lv[j].pid is None else lv[j].pid.data_ptr()
+    esz = 4 if T == torch.float32 else 8
+    hs = (kt.data_ptr(), om.data_ptr(), nt, hw.data_ptr(), nl)
+    fa = rng.standard_normal((B, lv[0].H, lv[0].W))
+    fa[:, 0] = fa[:, -1] = fa[:, :, 0] = fa[:, :, -1] = 0
+
+    def reset():
+        put(lv[0], "f", fa)
+        for j in range(3):
+            if j:
+                put(lv[j], "f", np.full((B, lv[j].H, lv[j].W), 5.0))
+            put(lv[j], "a", np.zeros((B, lv[j].H, lv[j].W)))
+            put(lv[j], "b", np.full((B, lv[j].H, lv[j].W), 7.0))
+
+    reset()  # per-level reference, down
+    for j in range(2):
+        _lib.call("mg_hsweep_restrict", T, None, None, lv[j].f.data_ptr(), lv[j].a.data_ptr(), lv[j + 1].f.data_ptr(),
+                  pid(j), *hs, rt.data_ptr(), nt, 1.25, *lv[j].geom(), lv[j + 1].ld, lv[j + 1].bs, None)
+    ref_down = [get(lv[0], "a"), get(lv[1], "f"), get(lv[1], "a"), get(lv[2], "f")]
+    # up from those iterates: e = a random coarse correction with a zero boundary
+    e = rng.standard_normal((B, lv[2].H, lv[2].W))
+    e[:, 0] = e[:, -1] = e[:, :, 0] = e[:, :, -1] = 0
+    put(lv[2], "b", e)
+    put(lv[1], "b", np.zeros((B, lv[1].H, lv[1].W)))  # (the solver's coarse buffers hold 0 on the boundary)
+    pp = (pt.data_ptr(), nt, 0.75)
+    _lib.call("mg_prolong_hsweep", T, lv[1].a.data_ptr(), None, lv[2].b.data_ptr(), lv[1].f.data_ptr(),
+              lv[1].b.data_ptr(), pid(1), pid(2), *hs, *pp, *lv[1].geom(), lv[2].ld, lv[2].bs, None)
+    put(lv[0], "b", np.full((B, lv[0].H, lv[0].W), 7.0))
+    _lib.call("mg_prolong_hsweep", T, lv[0].a.data_ptr(), None, lv[1].b.data_ptr(), lv[0].f.data_ptr(),
+              lv[0].b.data_ptr(), pid(0), pid(1), *hs, *pp, *lv[0].geom(), lv[1].ld, lv[1].bs, None)
+    ref_up = get(lv[0], "b")
+    pids_arr = _lib.PtrArray([pid(j) for j in range(3)]) if nt > 1 else None
+    fs = _lib.PtrArray([l.f.data_ptr() for l in lv])
+    tds = [t for t in (16, 8, 4, 2) if _lib.hmid_lds_bytes(False, t, nl, esz, nt > 1) > 0]
+    tus = [t for t in (64, 32, 16, 8) if _lib.hmid_lds_bytes(True, t, nl, esz, nt > 1) > 0]
+    assert tds and tus
+    for td in tds:
+        reset()
+        _lib.call("mg_hmid_down", T, fs, _lib.PtrArray([lv[0].a.data_ptr(), lv[1].a.data_ptr()]), pids_arr, B,
+                  lv[0].H, lv[0].W, *hs, rt.data_ptr(), nt, 1.25, td, None)
+        got = [get(lv[0], "a"), get(lv[1], "f"), get(lv[1], "a"), get(lv[2], "f")]
+        for k, (g_, r_) in enumerate(zip(got, ref_down)):
+            assert torch.equal(g_, r_), (td, k, (g_ - r_).abs().max().item())
+    put(lv[2], "b", e)
+    for tu in tus:
+        put(lv[0], "b", np.full((B, lv[0].H, lv[0].W), 7.0))
+        _lib.call("mg_hmid_up", T, _lib.PtrArray([lv[0].f.data_ptr(), lv[1].f.data_ptr()]),
+                  _lib.PtrArray([lv[0].a.data_ptr(), lv[1].a.data_ptr()]), lv[2].b.data_ptr(), lv[0].b.data_ptr(),
+                  pids_arr, B, lv[0].H, lv[0].W, *hs, *pp, tu, None)
+        got = get(lv[0], "b")
+        assert torch.equal(got, ref_up), (tu, (got - ref_up).abs().max().item())
+        assert (got[:, 0] == 7).all() and (got[:, -1] == 7).all() and (got[:, :, 0] == 7).all()
