@@ -26,6 +26,12 @@ constexpr int kHMaxLayers = 3;    // HNet(nb_layers=3) (M-FEANet-mg_test.ipynb:2
 #endif
 constexpr int kHPrefetch = FEA_HSWEEP_PF;
 static_assert(kHPrefetch == 1 || kHPrefetch == 2, "hsweep prefetch of 1 or 2 rows");
+// rows in flight of the sweep + restriction kernel with the 6-step loop body (the fine level's, 227 -> 231 VGPRs, two
+// waves per SIMD either way): 3 -> 4097^2 fp64 111.4 -> 106.0 us (same lease, profiles/r05_hjac/prefetch3_ab.txt).
+// The prolongation variant stays at 2 (3 spills it at its three-wave register cap).
+#ifndef FEA_HSWEEP_PF6
+#define FEA_HSWEEP_PF6 3
+#endif
 constexpr int kHTS = 10;          // LDS table stride (9 weights + omega/d)
 // Weights: the stencil / HNet / transfer weights (up to 46 doubles: more than the SGPR file holds beside the
 // kernel's addresses) are re-read with scalar loads at every row step, stage by stage, each stage's loads held
@@ -337,7 +343,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   // input rows PF steps ahead, in a ring of PF slots indexed by the step's position (compile-time after the
   // unroll below): step y consumes u(y), pid(y), f(y-1) (RAW: u_raw(y-1); MODE 2: f and pid of its residual row
   // y-2-NL, the iterate of its out row y-1-NL) and refills the slot with the rows of step y+PF at once
-  constexpr int PF = kHPrefetch;
+  constexpr int PF = (MODE == 2 && hs_unroll_steps<T, MULTI, MODE, ZERO, RAW>() == 6) ? FEA_HSWEEP_PF6 : kHPrefetch;
   T ur[PF][V], fr_[PF][V], rw_[PF][V], frr[PF][V], uo[PF][V];
   int pr[PF][V], po[PF][V];
   // MODE 2 needs the iterate's values of an out row only where they stand in for the sweep (boundary nodes)
