@@ -9,5 +9,5 @@ done; done
 i=0
 for L in "$@"; do i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $T/v$i -o run -- python3 tools/lab/with_lib.py $L bench.py --smoother hjac --steps 200 --warmup 5 --no-cpu-baseline --kernel-reps 3 > $T/v$i.json 2> $T/v$i.err || { tail $T/v$i.err; exit 1; }
-  python3 tools/trace_summary.py $T/v$i > $T/v$i.txt; echo "== $L"; head -4 $T/v$i.txt
+  python3 tools/trace_summary.py $T/v$i > $T/v$i.txt; echo "== $L"; head -9 $T/v$i.txt
 done
