@@ -29,10 +29,14 @@ the metric configuration (4097^2, one GPU, no decomposition).  Timing: barrier +
 sides of the K steps, max over ranks.
 """
 import argparse
+import contextlib
+import faulthandler
 import json
 import os
 import sys
+import threading
 import time
+from datetime import timedelta
 
 import numpy as np
 import torch
@@ -49,27 +53,93 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_init(force=False, backend="nccl"):
+EXIT_HANG = 3  # a bounded phase ran out of time (PhaseGuard)
+
+
+def dist_init(force=False, backend="nccl", timeout_s=150.0, cuda=True):
     """One process per GPU (torchrun env).  force: create the process group even for one rank (the
     domain-decomposed path always talks through torch.distributed).  backend "gloo": rehearsal of the
-    multi-rank path with several processes on one GPU (RCCL refuses two ranks on one device)."""
+    multi-rank path with several processes on one GPU (RCCL refuses two ranks on one device).  timeout_s: the
+    process group's collective timeout (both backends; with RCCL async error handling on, a collective stuck
+    past it aborts the communicator and ends the process instead of waiting for the 10-minute default)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if backend == "gloo":  # rehearsal: more ranks than GPUs share them
-        local %= max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    if cuda:
+        if backend == "gloo":  # rehearsal: more ranks than GPUs share them
+            local %= max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
     if ws > 1 or force:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(ws))
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        to = timedelta(seconds=timeout_s)
         if backend == "gloo":
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
     return ws, rank
+
+
+class PhaseGuard:
+    """Bounded phases of a run, one guard per rank.  A phase that outlives its limit — a collective that a peer
+    never entered, a captured RCCL block whose messages never complete — ends THIS process (os._exit, never an
+    exec) instead of holding every rank until the driver's timeout: the guard's thread names the rank and the
+    phase on stderr, dumps every thread's stack, runs the phase's on_expire (which may print the record so far
+    and choose the exit status; default EXIT_HANG) and exits.  Collectives and graph replays release the GIL, so
+    the thread runs while the main thread waits in one; faulthandler's own timer (no GIL needed) backs it up
+    30 s later.  Every rank guards the same phases, so a hang in a collective ends all of them."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.cv = threading.Condition()
+        self.cur = None  # (name, deadline, seconds, on_expire)
+        threading.Thread(target=self._watch, daemon=True, name="bench-phase-guard").start()
+
+    @contextlib.contextmanager
+    def phase(self, name, seconds, on_expire=None):
+        with self.cv:
+            prev = self.cur
+            self.cur = (name, time.monotonic() + seconds, seconds, on_expire)
+            self.cv.notify_all()
+        faulthandler.dump_traceback_later(seconds + 30, exit=True)
+        try:
+            yield
+        finally:
+            faulthandler.cancel_dump_traceback_later()
+            with self.cv:
+                self.cur = prev
+                self.cv.notify_all()
+            if prev is not None:
+                faulthandler.dump_traceback_later(max(1.0, prev[1] - time.monotonic()) + 30, exit=True)
+
+    def _watch(self):
+        with self.cv:
+            while True:
+                if self.cur is None:
+                    self.cv.wait()
+                    continue
+                left = self.cur[1] - time.monotonic()
+                if left > 0:
+                    self.cv.wait(left)
+                    continue
+                name, _, seconds, on_expire = self.cur
+                break
+        log(f"[bench] rank {self.rank}: phase '{name}' did not finish within {seconds:.0f} s (a collective or "
+            f"communication step some rank never completed); exiting")
+        faulthandler.dump_traceback(all_threads=True)
+        code = EXIT_HANG
+        if on_expire is not None:
+            try:
+                code = on_expire(name, seconds)
+            except BaseException as e:  # the exit must happen whatever the callback does
+                log(f"[bench] rank {self.rank}: on_expire failed: {e!r}")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(code)
 
 
 def barrier(ws):
@@ -310,37 +380,49 @@ def single_gpu_same_grid(m, n, T, B, steps, ms_dd):
             "workload": f"{m + 1}x{n + 1} poisson V-cycle on one GPU (MultigridSolver, no decomposition), rank 0"}
 
 
-def dd_parity_check(s, m, n, T, B, ws, cycles=3):
-    """Every rank: the decomposed solver's owned block after `cycles` V-cycles from zero against the single-GPU
-    MultigridSolver's on the same global grid and seeded rhs (run on the rank's own GPU).  The decomposed
-    cycle is bitwise the single-GPU one by construction (tests/test_gpu_dd.py); this puts that claim on the
-    line of every multi-GPU run, i.e. on the RCCL path itself.  Returns the max over ranks of the largest
-    absolute difference and of the count of differing nodes."""
+def dd_reference_block(owned, m, n, T, B, cycles=3):
+    """The single-GPU MultigridSolver's iterate after `cycles` V-cycles from zero on the decomposed run's global grid
+    and seeded rhs, cut to this rank's owned block ((y0, y1), (x0, x1)); run on the rank's own GPU, no
+    communication.  The reference point of every dd mode's parity check."""
     from feanet_amd.solver import MultigridSolver
+    (y0, y1), (x0, x1) = owned
     g = torch.Generator(device="cuda")
     g.manual_seed(1234)
     f = torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g)
-    s.load()
-    s.vcycle(cycles)
-    (y0, y1), (x0, x1), u = s.owned_block()
     ref = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B)
     ref.set_rhs(f=f)
     del f
     ref.load()
     ref.vcycle(cycles)
-    exp = ref.solution()[:, :, y0:y1, x0:x1]
-    diff = (u - exp).abs()
-    gloo = ws > 1 and torch.distributed.get_backend() != "nccl"  # gloo reduces host tensors (max_over_ranks)
-    out = torch.tensor([diff.max().item(), float((u != exp).sum().item())], dtype=torch.float64,
-                       device="cpu" if gloo else "cuda")
-    del ref, exp, diff, u
+    exp = ref.solution()[:, :, y0:y1, x0:x1].clone()
+    del ref
     torch.cuda.empty_cache()
+    return exp
+
+
+def dd_parity(s, exp, m, n, ws, cycles=3, repeats=3):
+    """Every rank: the decomposed solver's owned block after `cycles` V-cycles from zero against the single-GPU
+    solver's (dd_reference_block), `repeats` times from a fresh load — the first run of a program is eager, the
+    second captures its blocks (capturing communicators) and replays them, the third replays — so the check covers
+    the path the timed cycles took.  The decomposed cycle is bitwise the single-GPU one by construction
+    (tests/test_gpu_dd.py); this puts that claim on the line of every multi-GPU run, i.e. on the RCCL path itself.
+    Returns the max over ranks and repeats of the largest absolute difference and of the count of differing nodes."""
+    dmax, nbad = 0.0, 0.0
+    for _ in range(repeats):
+        s.load()
+        s.vcycle(cycles)
+        _, _, u = s.owned_block()
+        dmax = max(dmax, (u - exp).abs().max().item())
+        nbad = max(nbad, float((u != exp).sum().item()))
+        del u
+    gloo = ws > 1 and torch.distributed.get_backend() != "nccl"  # gloo reduces host tensors
+    out = torch.tensor([dmax, nbad], dtype=torch.float64, device="cpu" if gloo else "cuda")
     if ws > 1:
         torch.distributed.all_reduce(out, op=torch.distributed.ReduceOp.MAX)
-    return {"cycles": cycles, "bitwise_equal": bool(out[1].item() == 0), "max_abs_diff": out[0].item(),
-            "max_differing_nodes_per_rank": int(out[1].item()),
+    return {"cycles": cycles, "repeats": repeats, "bitwise_equal": bool(out[1].item() == 0),
+            "max_abs_diff": out[0].item(), "max_differing_nodes_per_rank": int(out[1].item()),
             "against": f"single-GPU MultigridSolver on the same {m + 1}x{n + 1} grid, V-cycles from zero, every "
-                       f"rank's owned block"}
+                       f"rank's owned block, {repeats} runs (eager / captured / replayed)"}
 
 
 def dd_domain(P, n0):
@@ -352,11 +434,15 @@ def dd_domain(P, n0):
     return n0 * P, n0
 
 
-def launch_ranks(n):
+def launch_ranks(n, timeout_s):
     """`bench.py --gpus N` (N > 1) started without a launcher: run the same command line under
     torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a CHILD process — nothing here has
     touched the GPU, and the process is not replaced (no exec) — forward its one JSON line to stdout (anything
-    else it printed there goes to stderr) and return its exit status."""
+    else it printed there goes to stderr) and return its exit status.  The child gets timeout_s in all (the
+    ranks bound their own phases well inside it, PhaseGuard); past it the launcher's process group is killed and
+    the status is EXIT_HANG.  The port is picked by binding port 0 and released just before the launch (a small
+    window in which another process could take it; the rendezvous then fails loudly, it does not hang)."""
+    import signal
     import socket
     import subprocess
     sk = socket.socket()
@@ -366,18 +452,315 @@ def launch_ranks(n):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     log(f"[bench] --gpus {n} without a launcher: {' '.join(cmd)}")
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
-    lines = r.stdout.splitlines()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+        rc = p.returncode
+    except subprocess.TimeoutExpired:
+        log(f"[bench] the {n} ranks did not finish within {timeout_s:.0f} s: killing them")
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        rc = EXIT_HANG
+    lines = out.splitlines()
     recs = [ln for ln in lines if ln.startswith("{")]
     for ln in lines:
         if not ln.startswith("{"):
             log(ln)
     if recs:
         print(recs[-1], flush=True)
-    if r.returncode == 0 and len(recs) != 1:
+    if rc == 0 and len(recs) != 1:
         log(f"[bench] expected one JSON line from rank 0, got {len(recs)}")
         return 1
-    return r.returncode
+    return rc
+
+
+def selftest_hang(args):
+    """--selftest-hang S (CPU, gloo, >= 2 ranks): rank 1 never enters the barrier rank 0 waits in, under the same
+    process-group timeout and PhaseGuard the GPU path uses (limit S), so the run must end non-zero within about S
+    seconds with the rank and phase named on stderr (tests/test_bench_cli.py)."""
+    ws, rank = dist_init(force=True, backend="gloo", timeout_s=4 * args.selftest_hang, cuda=False)
+    guard = PhaseGuard(rank)
+    import torch.distributed as dist
+    with guard.phase("selftest: barrier that rank 1 skips", args.selftest_hang):
+        if rank == 1:
+            time.sleep(10 * args.selftest_hang)
+        dist.barrier()
+    return 0
+
+
+# domain-decomposition modes timed on every N > 1 line, safest first: (name, whole-cycle capture, level-0 halo
+# overlapped with the coarse levels, finest join split into border rectangles + the exchange on a side stream)
+DD_MODES = [("segments", False, False, False), ("segments+overlap_l0", False, True, False),
+            ("segments+split_join", False, False, True), ("captured", True, False, False),
+            ("captured+overlap_l0", True, True, False), ("captured+split_join", True, False, True)]
+
+
+def time_steps(s, steps, warmup, ws):
+    """The contract's timing: warm-up calls of the timed call itself (vcycle(steps)), so that every graph the timed
+    call replays (its blocks of joined cycles, keyed by start buffer and size; 6 calls cover every step count) has
+    run once eagerly and been captured before the clock starts — at least `warmup` cycles; then barrier +
+    synchronize, ONE vcycle(steps), synchronize + barrier, max over ranks.  Returns (seconds, warm-up cycles run)."""
+    calls = max(6, -(-warmup // steps))
+    calls += calls % 2
+    for _ in range(calls):
+        s.vcycle(steps)
+    torch.cuda.synchronize()
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.vcycle(steps)
+    torch.cuda.synchronize()
+    barrier(ws)
+    torch.cuda.synchronize()
+    return max_over_ranks(time.perf_counter() - t0, ws), calls * steps
+
+
+def contraction(s):
+    """Residual contraction factor per cycle over the first 8 cycles from zero (before the fp64 floor)."""
+    s.load()
+    r0 = s.residual_norm()
+    s.vcycle(8)
+    conv = float((s.residual_norm().max() / r0.max()).item()) ** (1.0 / 8)
+    s.load()
+    return conv
+
+
+def roofline_record(fine, lvl, args, jt=None, jsrc=None, dom=None, tkey_ok=False, ws=1):
+    """The `roofline` and `north_star_kernel` objects from the fine-level kernel timings (see the module doc)."""
+    L0 = lvl.levels[0]
+    kt, kbytes = fine["fea_mg_sweep"]
+    kt = max_over_ranks(kt, ws)
+    if dom is not None:
+        name, r_t, r_bytes = dom
+        rkern = (f"{name} (fine level {L0.H}x{L0.W} {args.dtype}; the slowest launch of the cycle, which joins no "
+                 f"cycles)")
+        tkey, jsrc = None, ("HIP events on the solver's stream between consecutive launches of eager replays of the "
+                            "V-cycle plan")
+    else:
+        if jt is None and "fea_mg_cycle_join" in fine:
+            jt = fine["fea_mg_cycle_join"][0]
+            jsrc = "HIP events, back-to-back launches of fea_mg_cycle_join on the level-0 buffers"
+        if jt is not None:
+            r_bytes = fine["fea_mg_cycle_join"][1]
+            r_t = max_over_ranks(jt, ws)
+            rkern = f"fea_mg_cycle_join (fine level {L0.H}x{L0.W} {args.dtype}: post-sweep of cycle k + pre-sweep, " \
+                    f"residual and restriction of cycle k+1 in one pass)"
+            tkey = "mg_cycle_join_f64_4097"
+        else:
+            rkern, r_t, r_bytes, tkey, jsrc = (f"fea_mg_sweep ({L0.H}x{L0.W} {args.dtype})", kt, kbytes,
+                                               "mg_sweep_f64_4097", "HIP events, back-to-back launches")
+    achieved = r_bytes / r_t / 1e9
+    traffic, tsrc = load_traffic(tkey) if (tkey_ok and tkey) else (None, None)
+    ns_traffic, ns_src = load_traffic("mg_sweep_f64_4097") if tkey_ok else (None, None)
+    roof = {"bound": "hbm", "kernel": rkern, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": r_t * 1e6,
+            "algorithmic_bytes_per_launch": r_bytes, "timing": jsrc}
+    ns = {"kernel": f"fea_mg_sweep (fine-level Ke-stencil Jacobi sweep, {L0.H}x{L0.W} {args.dtype}, 24 B/node)",
+          "achieved": kbytes / kt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kbytes / kt / 1e9 / HBM_PEAK_GBS,
+          "avg_launch_us": kt * 1e6, "algorithmic_bytes_per_launch": kbytes, "traffic": ns_traffic,
+          "traffic_source": ns_src, "target_frac": 0.70}
+    fl = {k: {"avg_launch_us": tk * 1e6, "algorithmic_bytes": nb, "achieved_GBps": nb / tk / 1e9,
+              "frac": nb / tk / 1e9 / HBM_PEAK_GBS} for k, (tk, nb) in fine.items()}
+    return roof, ns, fl
+
+
+def base_record(args, value, ms_step, ws, warm, workload, mode, parallelism, rhs, levels, B):
+    return {
+        "metric": METRIC,
+        "value": value,
+        "unit": "DoF-updates/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "warmup_executed_steps": warm,
+        "warmup_note": ("warmup = the requested --warmup; warmup_executed_steps = the untimed cycles actually run "
+                        "before the clock (>= warmup: whole calls of the timed vcycle(steps), so every HIP graph it "
+                        "replays is captured before timing)"),
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong" if (mode == "dd" and not args.weak) else "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": {"randn": "synthetic (seeded Gaussian rhs, zero initial guess)",
+                 "ones": "synthetic (uniform nodal source F = ones, FNet applied, as MM_Interface_error.ipynb; zero "
+                         "initial guess)",
+                 "families": "synthetic (nodal sources from the six Data/RHS/generate_rhs.py families, seeded, FNet "
+                             "applied; zero initial guess)"}[rhs],
+        "config": {"workload": workload, "mode": mode, "batch": B, "levels": levels, "parallelism": parallelism},
+    }
+
+
+def run_dd(args, ws, rank, T, B, guard, emit):
+    """The N > 1 line: ONE global grid domain-decomposed over the ranks (feanet_amd.dd), every DD mode of DD_MODES
+    selected by --dd-modes timed in turn on the live communicator (each its own solver, warm-up and K timed cycles,
+    and its own bitwise dd_parity), each under a bounded phase.  The line's headline (value, ms_per_step,
+    config.dd_mode, dd_parity) is the FASTEST mode whose parity is bitwise; every mode is listed under dd_modes.
+    The first mode is required (any failure ends the run non-zero); a later mode that fails is recorded and skipped,
+    and one that hangs past --mode-timeout ends the run with the record so far printed (exit 0: the headline was
+    measured on modes that completed; the hung one is named in dd_modes)."""
+    from feanet_amd.dd import DDSolver, TorchComm, default_grid
+    if args.weak:
+        m, nc = dd_domain(ws, args.n)
+    else:
+        m = nc = args.global_n or 8192
+    grid = tuple(int(x) for x in args.grid.lower().split("x")) if args.grid else default_grid(ws)
+    wanted = [x.strip() for x in args.dd_modes.split(",")] if args.dd_modes != "all" else [x[0] for x in DD_MODES]
+    modes = [md for md in DD_MODES if md[0] in wanted]
+    if args.backend != "nccl":  # capture needs device communication (gloo stages through the host)
+        modes = [md for md in modes if not md[1]]
+    if not modes:
+        raise SystemExit(f"bench: no dd mode selected from {args.dd_modes!r} for backend {args.backend}")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)  # one global problem: every rank draws the same rhs and keeps its block
+    f = torch.randn(B, 1, m + 1, nc + 1, device="cuda", dtype=T, generator=g)
+    dof = B * (m + 1) * (nc + 1)
+    rec, exp, results = None, None, []
+
+    def expire(name, seconds):  # a mode after the first hung: print what was measured, name the hung mode
+        if rec is None:
+            return EXIT_HANG
+        rec["dd_modes"].append({"mode": name.split(" ")[-1], "status": f"did not finish within {seconds:.0f} s on "
+                                f"rank {rank} (phase '{name}'); every rank exited"})
+        if rank == 0:
+            emit(rec)
+        return 0
+
+    for i, (name, cap, ov, sj) in enumerate(modes):
+        t0 = time.perf_counter()
+        try:
+            with guard.phase(f"dd mode {name}", args.mode_timeout, None if i == 0 else expire):
+                s = DDSolver(nc, m, rank, ws, comm=TorchComm(capture=cap), agglomerate=args.agglomerate, dtype=T,
+                             batch=B, grid=grid, overlap_l0=ov, split_join=sj)
+                s.set_rhs(f)
+                s.load()
+                conv = contraction(s) if i == 0 else None
+                t, warm = time_steps(s, args.steps, args.warmup, ws)
+                captured = bool(s.comm.capturable and s._capture_ok and s.use_graph)
+                par = None
+                if not args.no_dd_parity:
+                    if exp is None:
+                        exp = dd_reference_block(s.owned_block()[:2], m, nc, T, B)
+                    par = dd_parity(s, exp, m, nc, ws)
+                    if cap:
+                        captured = captured and bool(s._capture_ok)
+        except Exception as e:
+            if i == 0:
+                raise
+            log(f"[bench] rank {rank}: dd mode {name} failed: {e!r}")
+            rec["dd_modes"].append({"mode": name, "status": f"error: {str(e)[:300]}"})
+            torch.cuda.synchronize()
+            continue
+        ms = t / args.steps * 1e3
+        r = {"mode": name, "status": "ok", "ms_per_step": ms, "value": dof / (t / args.steps),
+             "cycle_graphs": ("captured (kernels + RCCL calls, one HIP graph per block of up to "
+                              f"{s.GRAPH_CYCLES} cycles)") if captured else
+                             ("segments (one HIP graph per kernel segment between communication steps)" if not cap else
+                              "segments (capture requested, refused on some rank: all ranks fell back)"),
+             "capture_requested": cap, "overlap_l0": ov, "split_join": sj, "backend": args.backend,
+             "dd_parity": par, "mode_seconds": round(time.perf_counter() - t0, 2)}
+        results.append(r)
+        if i == 0:
+            fine = time_fine_kernels(s.local, args.kernel_reps)
+            roof, ns, fl = roofline_record(fine, s.local, args, ws=ws)
+            p0, q0 = s.parts[0], s.cparts[0]
+            workload = (f"{m + 1}x{nc + 1} poisson {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
+                        f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
+                        f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
+                        + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))
+            parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (one phase, packed, depths "
+                           f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
+            rec = base_record(args, r["value"], ms, ws, warm, workload, "dd", parallelism, "randn", s.L, B)
+            rec.update({"roofline": roof, "north_star_kernel": ns, "fine_level_kernels": fl,
+                        "vcycle_hbm_gbps_algorithmic": None, "vcycle_algorithmic_bytes": None,
+                        "residual_contraction_per_cycle": conv, "dd_modes": results, "cpu_baseline": None})
+            if ws > 1:
+                # the same global grid on ONE GPU (rank 0; the others wait at the barrier): the strong-scaling base
+                # point of this line, so speed-up and efficiency follow from the line itself
+                del s
+                torch.cuda.empty_cache()
+                with guard.phase("single-GPU base point (rank 0) + barrier", args.mode_timeout):
+                    if rank == 0:
+                        rec["single_gpu_same_grid"] = single_gpu_same_grid(m, nc, T, B, args.steps, ms)
+                    barrier(ws)
+        ok = [x for x in results if x["status"] == "ok" and (x["dd_parity"] is None or x["dd_parity"]["bitwise_equal"])]
+        best = min(ok, key=lambda x: x["ms_per_step"]) if ok else results[0]
+        rec["value"], rec["ms_per_step"] = best["value"], best["ms_per_step"]
+        rec["headline_mode"] = best["mode"]
+        rec["config"]["dd_mode"] = {k: best[k] for k in ("mode", "cycle_graphs", "capture_requested", "overlap_l0",
+                                                         "split_join", "backend")}
+        rec["config"]["parallelism"] = rec["config"]["parallelism"].split("; headline mode")[0] + \
+            f"; headline mode {best['mode']} (fastest bitwise of {len(results)} timed)"
+        if best["dd_parity"] is not None:
+            rec["dd_parity"] = best["dd_parity"]
+        if "single_gpu_same_grid" in rec:
+            rec["single_gpu_same_grid"]["speedup_of_this_line"] = \
+                rec["single_gpu_same_grid"]["ms_per_step"] / best["ms_per_step"]
+        if "s" in locals():
+            del s
+        torch.cuda.empty_cache()
+    return rec
+
+
+def run_single(args, ws, rank, T, B):
+    """N = 1 (or --mode replicas): the metric configuration by default — one 4097^2 fp64 Poisson problem per GPU."""
+    from feanet_amd.solver import MultigridSolver
+    n = args.n
+    N = n + 1
+    rhs = args.rhs or ("families" if B > 1 else "ones" if args.problem == "interface" else "randn")
+    hnet, kw = None, {}
+    wdir = os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights")
+    if args.smoother == "hjac":
+        w = np.load(os.path.join(wdir, "hnet_iso_poisson_33x33.npz"))
+        hnet = np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+    learned = args.problem == "interface" and args.transfer == "learned"
+    if learned:  # BASELINE C3: FEANet/multigrid.py's trained ratio R / P / w (MM_Interface_error.ipynb)
+        w = np.load(os.path.join(wdir, "multigrid_interface_ratio.npz"))
+        kw = dict(R=w["R"][0], P=w["P"][:, 0], w=w["w"])
+    s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B, levels=args.levels, smoother=args.smoother,
+                        hnet=hnet, **kw)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    if rhs == "families":
+        from tools import rhs_families
+        s.set_rhs(F=rhs_families.batch(B, N, T, "cuda", seed=rank))
+    elif rhs == "ones":
+        s.set_rhs(F=torch.ones(B, 1, N, N, device="cuda", dtype=T))
+    else:
+        s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
+    dof = B * N * N * ws
+    workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics"
+                f"{', learned HRelax smoother' if args.smoother == 'hjac' else ''}"
+                f"{', learned ratio R/P/w of FEANet/multigrid.py (BASELINE C3)' if learned else ''}), batch {B} per GPU")
+    parallelism = "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"
+    s.load()
+    conv = contraction(s)
+    t, warm = time_steps(s, args.steps, args.warmup, ws)
+    ms_step = t / args.steps * 1e3
+    rec = base_record(args, dof / (t / args.steps), ms_step, ws, warm, workload, "single" if ws == 1 else "replicas",
+                      parallelism, rhs, s.L, B)
+    fine = time_fine_kernels(s, args.kernel_reps)
+    L0 = s.levels[0]
+    metric_cfg = (L0.H == 4097 and L0.W == 4097 and B == 1 and args.dtype == "f64" and args.problem == "poisson")
+    # roofline: the DOMINANT kernel of the timed region — the finest level's cycle join (one per V-cycle
+    # boundary, ~45 % of the V-cycle), timed inside the cycle with HIP events on the solver's stream
+    jt = time_join_in_cycle(s, min(args.steps, 200))
+    jsrc = ("HIP events in the solver's stream, eager replays of vcycle(K): [previous launch + join] minus "
+            "[previous launch] per cycle")
+    dom = time_fine_launch_in_cycle(s) if (jt is None and not s._joinable()) else None
+    roof, ns, fl = roofline_record(fine, s, args, jt=jt, jsrc=jsrc, dom=dom, tkey_ok=(ws == 1 and metric_cfg), ws=ws)
+    vbytes = s.bytes_per_vcycle(args.steps)
+    rec.update({"roofline": roof, "north_star_kernel": ns, "fine_level_kernels": fl,
+                "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if (ws == 1 and vbytes) else None,
+                "vcycle_algorithmic_bytes": vbytes, "residual_contraction_per_cycle": conv})
+    if args.problem == "interface":
+        rec["config"]["transfer"] = ("learned ratio R/P/w (feanet_amd/weights/multigrid_interface_ratio.npz)" if learned
+                                     else "linear (the reference's default RestrictionNet / ProlongationNet)")
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.problem == "poisson" and B == 1:
+        log("[bench] timing the CPU oracle baseline ...")
+        rec["cpu_baseline"] = cpu_baseline(n)
+    else:
+        rec["cpu_baseline"] = None
+    return rec
 
 
 def main():
@@ -402,10 +785,22 @@ def main():
     ap.add_argument("--weak", action="store_true",
                     help="dd: weak scaling instead, --n x --n intervals per GPU (4097^2, 8193x4097, 8193^2, 16385x8193)")
     ap.add_argument("--grid", default=None, help="dd: rank grid PRxPC (default: 2->2x1, 4->2x2, 8->4x2)")
-    ap.add_argument("--rhs", default=None, choices=["randn", "families"],
-                    help="right-hand side: seeded Gaussian assembled rhs, or nodal sources from the six "
-                         "families of the reference's Data/RHS/generate_rhs.py with FNet applied (default: "
-                         "families for batches, the BASELINE C5 inputs; randn otherwise)")
+    ap.add_argument("--dd-modes", default="all",
+                    help="dd: comma list of modes to time (" + ", ".join(x[0] for x in DD_MODES) + ") or all; the "
+                         "captured ones need --backend nccl")
+    ap.add_argument("--mode-timeout", type=float, default=120.0,
+                    help="dd: seconds one mode (build, warm-up, timed cycles, parity) may take on a rank")
+    ap.add_argument("--dist-timeout", type=float, default=150.0, help="process-group collective timeout (s)")
+    ap.add_argument("--launch-timeout", type=float, default=560.0,
+                    help="--gpus N without a launcher: seconds the N ranks may take in all")
+    ap.add_argument("--rhs", default=None, choices=["randn", "families", "ones"],
+                    help="right-hand side: seeded Gaussian assembled rhs, nodal sources from the six families of the "
+                         "reference's Data/RHS/generate_rhs.py with FNet applied, or F = ones with FNet applied "
+                         "(default: families for batches, the BASELINE C5 inputs; ones for the interface problem, "
+                         "BASELINE C3; randn otherwise)")
+    ap.add_argument("--transfer", default="learned", choices=["learned", "linear"],
+                    help="interface problem: the trained ratio R/P/w of FEANet/multigrid.py (BASELINE C3, default) or "
+                         "the linear transfer operators")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dd-parity", action="store_true",
                     help="dd: skip the per-rank bitwise check against a global-grid single-GPU solver (it holds the "
@@ -413,199 +808,45 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend (gloo: multi-process rehearsal on one GPU, host-staged)")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--selftest-hang", type=float, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     env_ws = os.environ.get("WORLD_SIZE")
     if env_ws is None and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
+        sys.exit(launch_ranks(args.gpus, args.launch_timeout))
     if env_ws is not None and int(env_ws) != args.gpus:
         sys.exit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_ws} ranks; pass --gpus "
                  f"{env_ws} (or run without a launcher: bench.py --gpus N starts N ranks itself)")
+    if args.selftest_hang is not None:
+        sys.exit(selftest_hang(args))
     # stdout carries exactly ONE line, the JSON record: everything else a library writes to fd 1
     # (RCCL prints its version banner there when the communicator comes up) goes to stderr
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
+    printed = []
+
+    def emit(rec):
+        if not printed:
+            printed.append(True)
+            print(json.dumps(rec), file=json_out, flush=True)
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     mode = args.mode or ("dd" if ws > 1 else "single")
-    ws, rank = dist_init(force=(mode == "dd"), backend=args.backend)
-    from feanet_amd.solver import MultigridSolver
+    if mode == "dd" and args.problem != "poisson":
+        raise SystemExit("bench: the domain-decomposed path runs the Poisson problem")
+    ws, rank = dist_init(force=(mode == "dd"), backend=args.backend, timeout_s=args.dist_timeout)
+    guard = PhaseGuard(rank)
     T = torch.float64 if args.dtype == "f64" else torch.float32
-    n, B = args.n, args.batch
-    rhs = args.rhs or ("families" if B > 1 else "randn")
-    g = torch.Generator(device="cuda")
     if mode == "dd":
-        if args.problem != "poisson":
-            raise SystemExit("bench: the domain-decomposed path runs the Poisson problem")
-        from feanet_amd.dd import DDSolver, TorchComm, default_grid
-        if args.weak:
-            m, nc = dd_domain(ws, n)
-        else:
-            m = nc = args.global_n or 8192
-        grid = tuple(int(x) for x in args.grid.lower().split("x")) if args.grid else default_grid(ws)
-        s = DDSolver(nc, m, rank, ws, comm=TorchComm(), agglomerate=args.agglomerate, dtype=T, batch=B, grid=grid)
-        g.manual_seed(1234)  # one global problem: every rank draws the same rhs and keeps its rows
-        f = torch.randn(B, 1, m + 1, nc + 1, device="cuda", dtype=T, generator=g)
-        s.set_rhs(f)
-        del f
-        torch.cuda.empty_cache()
-        dof = B * (m + 1) * (nc + 1)
-        lvl = s.local
-        p0, q0 = s.parts[0], s.cparts[0]
-        workload = (f"{m + 1}x{nc + 1} poisson {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
-                    f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
-                    f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
-                    + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))
-        parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (one phase, packed, depths "
-                       f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
+        rec = run_dd(args, ws, rank, T, args.batch, guard, emit)
     else:
-        N = n + 1
-        hnet = None
-        if args.smoother == "hjac":
-            w = np.load(os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
-            hnet = np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
-        s = MultigridSolver(n, problem=args.problem, dtype=T, batch=B, levels=args.levels, smoother=args.smoother,
-                            hnet=hnet)
-        g.manual_seed(1234 + rank)
-        if rhs == "families":
-            from tools import rhs_families
-            s.set_rhs(F=rhs_families.batch(B, N, T, "cuda", seed=rank))
-        else:
-            s.set_rhs(f=torch.randn(B, 1, N, N, device="cuda", dtype=T, generator=g))
-        dof = B * N * N * ws
-        lvl = s
-        workload = (f"{N}x{N} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1) (MultiGrid.Step semantics"
-                    f"{', learned HRelax smoother' if args.smoother == 'hjac' else ''}), batch {B} per GPU")
-        parallelism = "replicas (one independent problem per GPU)" if ws > 1 else "single GPU"
-    s.load()
-    # contraction factor over the first 8 cycles (before the fp64 floor), then restart from zero
-    r0 = s.residual_norm()
-    s.vcycle(8)
-    conv = float((s.residual_norm().max() / r0.max()).item()) ** (1.0 / 8)
-    s.load()
-
-    # warm-up: the timed call itself (vcycle(steps)), repeated so that every graph the timed call
-    # replays (its blocks of joined cycles, keyed by start buffer and size; 5 calls cover every step
-    # count) has run once eagerly and been captured before the clock starts.  At least --warmup cycles.
-    calls = max(6, -(-args.warmup // args.steps))
-    calls += calls % 2
-    warm = 0
-    for _ in range(calls):
-        s.vcycle(args.steps)
-        warm += args.steps
-    torch.cuda.synchronize()
-    barrier(ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    s.vcycle(args.steps)
-    torch.cuda.synchronize()
-    barrier(ws)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    t = max_over_ranks(t, ws)
-    ms_step = t / args.steps * 1e3
-    value = dof / (t / args.steps)
-
-    fine = time_fine_kernels(lvl, args.kernel_reps)
-    L0 = lvl.levels[0]
-    metric_cfg = (L0.H == 4097 and L0.W == 4097 and B == 1 and args.dtype == "f64" and args.problem == "poisson")
-    # north-star kernel: the fine-level Ke-stencil Jacobi sweep on its own (back-to-back launches)
-    kt, kbytes = fine["fea_mg_sweep"]
-    kt = max_over_ranks(kt, ws)
-    # roofline: the DOMINANT kernel of the timed region — the finest level's cycle join (one per V-cycle
-    # boundary, ~45 % of the V-cycle), timed inside the cycle with HIP events on the solver's stream
-    jt = time_join_in_cycle(s, min(args.steps, 200)) if mode == "single" else None
-    jsrc = ("HIP events in the solver's stream, eager replays of vcycle(K): [previous launch + join] minus "
-            "[previous launch] per cycle")
-    dom = None
-    if jt is None and mode == "single" and not s._joinable():
-        dom = time_fine_launch_in_cycle(s)  # no join in this schedule: its own slowest fine-level launch
-    if dom is not None:
-        name, r_t, r_bytes = dom
-        rkern = (f"{name} (fine level {L0.H}x{L0.W} {args.dtype}; the slowest launch of the cycle, which joins no "
-                 f"cycles)")
-        tkey, jsrc = None, ("HIP events on the solver's stream between consecutive launches of eager replays of the "
-                            "V-cycle plan")
-    elif jt is None and "fea_mg_cycle_join" in fine:
-        jt = fine["fea_mg_cycle_join"][0]
-        jsrc = "HIP events, back-to-back launches of fea_mg_cycle_join on the level-0 buffers"
-    if dom is None and jt is not None:
-        jbytes = fine["fea_mg_cycle_join"][1] if "fea_mg_cycle_join" in fine else None
-        jt = max_over_ranks(jt, ws)
-        rkern = f"fea_mg_cycle_join (fine level {L0.H}x{L0.W} {args.dtype}: post-sweep of cycle k + pre-sweep, " \
-                f"residual and restriction of cycle k+1 in one pass)"
-        r_t, r_bytes, tkey = jt, jbytes, "mg_cycle_join_f64_4097"
-    elif dom is None:
-        rkern, r_t, r_bytes, tkey, jsrc = (f"fea_mg_sweep ({L0.H}x{L0.W} {args.dtype})", kt, kbytes,
-                                           "mg_sweep_f64_4097", "HIP events, back-to-back launches")
-    achieved = r_bytes / r_t / 1e9
-    traffic, tsrc = load_traffic(tkey) if (mode == "single" and metric_cfg) else (None, None)
-    ns_traffic, ns_src = load_traffic("mg_sweep_f64_4097") if (mode == "single" and metric_cfg) else (None, None)
-    vbytes = s.bytes_per_vcycle(args.steps) if mode == "single" else None
-    dd_mode = None
-    if mode == "dd":  # the path the timed cycles actually took (a refused capture falls back on every rank)
-        captured = bool(getattr(s.comm, "capturable", False) and s._capture_ok and s.use_graph)
-        dd_mode = {"cycle_graphs": "captured (kernels + RCCL calls, one HIP graph per block of up to "
-                                   f"{s.GRAPH_CYCLES} cycles)" if captured else "segments (one HIP graph per kernel "
-                                   "segment between communication steps)",
-                   "split_join": bool(s.split_join and captured), "overlap_l0": bool(s.overlap_l0),
-                   "backend": args.backend}
-        parallelism += (f"; cycles {'captured whole' if captured else 'in kernel segments'}, split_join "
-                        f"{dd_mode['split_join']}, overlap_l0 {dd_mode['overlap_l0']}")
-
-    rec = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "DoF-updates/s",
-        "n_gpus": ws,
-        "steps": args.steps,
-        "warmup": warm,
-        "ms_per_step": ms_step,
-        "higher_is_better": True,
-        "scaling": "strong" if (mode == "dd" and not args.weak) else "weak",
-        "vs_baseline": None,
-        "dtype": args.dtype,
-        "data": ("synthetic (seeded Gaussian rhs, zero initial guess)" if rhs == "randn" else
-                 "synthetic (nodal sources from the six Data/RHS/generate_rhs.py families, seeded, FNet applied; "
-                 "zero initial guess)"),
-        "config": {"workload": workload, "mode": mode, "batch": B, "levels": s.L, "parallelism": parallelism,
-                   **({"dd_mode": dd_mode} if dd_mode else {})},
-        "roofline": {"bound": "hbm", "kernel": rkern,
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": r_t * 1e6,
-                     "algorithmic_bytes_per_launch": r_bytes, "timing": jsrc},
-        "north_star_kernel": {"kernel": f"fea_mg_sweep (fine-level Ke-stencil Jacobi sweep, {L0.H}x{L0.W} "
-                                        f"{args.dtype}, 24 B/node)",
-                              "achieved": kbytes / kt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": kbytes / kt / 1e9 / HBM_PEAK_GBS, "avg_launch_us": kt * 1e6,
-                              "algorithmic_bytes_per_launch": kbytes, "traffic": ns_traffic,
-                              "traffic_source": ns_src, "target_frac": 0.70},
-        "fine_level_kernels": {k: {"avg_launch_us": tk * 1e6, "algorithmic_bytes": nb,
-                                   "achieved_GBps": nb / tk / 1e9, "frac": nb / tk / 1e9 / HBM_PEAK_GBS}
-                               for k, (tk, nb) in fine.items()},
-        "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if (ws == 1 and vbytes) else None,
-        "vcycle_algorithmic_bytes": vbytes,
-        "residual_contraction_per_cycle": conv,
-    }
-    if mode == "dd" and ws > 1:
-        # the same global grid on ONE GPU (rank 0; the others wait at the barrier): the strong-scaling base
-        # point of this line, so speed-up and efficiency follow from the line itself
-        if rank == 0:
-            rec["single_gpu_same_grid"] = single_gpu_same_grid(m, nc, T, B, args.steps, ms_step)
-        barrier(ws)
-    if mode == "dd" and not args.no_dd_parity:
-        rec["dd_parity"] = dd_parity_check(s, m, nc, T, B, ws)
-    if rank == 0 and ws == 1 and mode == "single" and not args.no_cpu_baseline and args.problem == "poisson" \
-            and B == 1:
-        log("[bench] timing the CPU oracle baseline ...")
-        rec["cpu_baseline"] = cpu_baseline(n)
-    elif rank == 0:
-        rec["cpu_baseline"] = None
+        rec = run_single(args, ws, rank, T, args.batch)
     if rank == 0:
-        print(json.dumps(rec), file=json_out, flush=True)
+        emit(rec)
     if torch.distributed.is_initialized():
-        torch.distributed.destroy_process_group()
+        with guard.phase("destroy_process_group", 60, lambda *_: 0):
+            torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -2980,6 +2980,9 @@ static void join_config(int B, int H, int W, MgArgs<T>& g) {
   g.nstrips = div_up(W - 2, Ovl3<T>::S);
   const int rb_pow2 = pick_rb(B, g.nstrips, H - 2, join_max_rb());
   g.rb = B >= kJoinBatchPow2 ? rb_pow2 : balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, rb_pow2);
+#ifdef FEA_LAB_JOIN_RB  // lab builds: a fixed task height (fine rows, even) for A/B runs
+  g.rb = FEA_LAB_JOIN_RB;
+#endif
   g.ntr = div_up((H + 1) / 2 - 2, g.rb / 2);
 }
 

@@ -58,7 +58,10 @@ def default_agglomeration(m, n, P, L, max_nodes=None, Pc=1):
     RCCL default) runs 267.0 / 160.7 us at Ld = 5 vs 285.6 / 167.5 at Ld = 4 on 2 / 4 ranks (the replicated coarse
     sub-cycle is shorter, the doubled ghost frames of the small levels cost less), and 116.7 at Ld = 4 vs 119.2 at
     Ld = 5 on 8, where the blocks are small enough that the doubled ghost frames cost more
-    (profiles/r05_dd/dd_projection.txt)."""
+    (profiles/r05_dd/dd_projection.txt).  Scope of that evidence: ONE grid (8193^2) and single-GPU projections whose
+    communicator moves nothing, so message and all-gather costs are not modelled; for other grids the rule is
+    only "stop coarsening the distributed levels once the global level is this small", pinned by
+    tests/test_dd.py for several sizes, not a measured optimum."""
     if max_nodes is None:
         max_nodes = (1 << 20) if P * Pc >= 8 else (1 << 18)
     Ld = 1
@@ -438,8 +441,9 @@ class DDSolver:
     the coarse solve) instead of with the coarse-level halo in one batch — one more message group and one
     more unpack launch per cycle; graph_min: kernel segments of fewer launches run eagerly instead of as HIP
     graphs (on this chip a graph launch between two communication steps costs ~8 us of GPU time, a short
-    eager segment less); split_join (captured cycles only): the finest join as border rectangles + the halo
-    exchange on a side stream beside the interior rectangle — off by default: on one GPU (8-rank projection,
+    eager segment less); split_join: the finest join as border rectangles + the halo exchange on a side stream
+    beside the interior rectangle (captured cycles: inside the block's graph; segment-wise: eager launches for that
+    segment) — off by default: on one GPU (8-rank projection,
     8193^2, 4x2) the split costs 142 instead of 117 us per cycle (thin border rectangles are mostly pipeline
     fill, the interior shares the CUs with them), more than an exchange of this size takes; overlap_l0
     overlaps the level-0 halo with the coarse levels instead; other args as MultigridSolver (Poisson).
@@ -853,8 +857,10 @@ class DDSolver:
         every capture the ranks agree (one all-reduce, outside the graph) whether ALL of them captured; if any
         refused, every rank discards its graphs and runs the segment-wise path from that block on — the same
         calls in the same order on every rank, so no message is left unmatched.  Only capture failures count as
-        a refusal (CUDA/HIP graph or stream-capture errors); any other error (e.g. an invalid kernel argument)
-        propagates."""
+        a refusal (_is_capture_error); any other error inside the capture (e.g. an invalid kernel argument) is
+        reported through the same all-reduce as an error and then raised on EVERY rank (the failing rank re-raises
+        its own exception, its peers a RuntimeError naming the failure count), so no rank is left waiting in a
+        collective its failed peer never enters."""
         i = 0
         while i < len(keys):
             key = keys[i]
@@ -873,18 +879,25 @@ class DDSolver:
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(stream)
-                ok = True
+                refused, error = False, None
                 try:
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         self._run_chunks(block, captured=True)
                 except RuntimeError as e:
-                    if not _is_capture_error(e):
-                        raise
-                    ok = False
+                    if _is_capture_error(e):
+                        refused = True
+                    else:
+                        error = e
                     g = None
                     torch.cuda.synchronize(self.device)
                 stream.wait_stream(s)
-                if not self._all_ranks_ok(ok):  # some rank refused: every rank leaves the captured path
+                n_refused, n_errors = self._agree(refused, error is not None)
+                if n_errors:  # every rank raises: the failing one its own error, the others name it
+                    if error is not None:
+                        raise error
+                    raise RuntimeError(f"DDSolver: {n_errors} peer rank(s) failed inside a captured block of "
+                                       f"cycles {block[0]}..{block[-1]} (rank {self.rank} aborts with them)")
+                if n_refused:  # some rank refused: every rank leaves the captured path
                     self._capture_ok = False
                     self._graphs = {k: v for k, v in self._graphs.items() if k[0] != "cap"}
                     self._run_chunks(keys[i:], captured=False)
@@ -895,13 +908,14 @@ class DDSolver:
                 g.replay()
             i += n
 
-    def _all_ranks_ok(self, ok):
-        """True iff `ok` holds on every rank (one all-reduce of the refusal count through the communicator)."""
+    def _agree(self, refused, failed):
+        """(ranks that refused the capture, ranks that failed with another error): one all-reduce of the two
+        counts through the communicator (this rank's own flags when it is alone)."""
         if getattr(self.comm, "world", 1) <= 1:
-            return ok
-        bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=self.device)
-        bad = self.comm.allreduce_sum(bad)
-        return float(bad.item()) == 0.0
+            return int(refused), int(failed)
+        t = torch.tensor([float(refused), float(failed)], dtype=torch.float64, device=self.device)
+        t = self.comm.allreduce_sum(t)
+        return int(t[0].item()), int(t[1].item())
 
     def _run_chunks(self, keys, captured=False):
         """Issue the chunks' kernel segments and communication steps in order on the current stream; captured:
@@ -917,8 +931,8 @@ class DDSolver:
                     if lvl0 and pending is not None:
                         self.comm.exchange_finish(pending)
                         pending = None
-                    if captured and self.split_join and self._split_join(segs, i):
-                        skip = i + 1  # the exchange ran beside the interior join
+                    if self.split_join and self._split_join(segs, i):
+                        skip = i + 1  # the exchange ran beside the interior join (eager launches off capture)
                     elif captured:
                         _launch_list(segs[i][1], self.dtype, torch.cuda.current_stream(self.device))
                     else:
@@ -1016,17 +1030,24 @@ class DDSolver:
         return torch.sqrt(n2)
 
 
+_CAPTURE_WORDS = ("operation not permitted when stream is capturing", "stream is capturing",
+                  "hiperrorstreamcapture", "cudaerrorstreamcapture", "hiperrorcapturedevent", "cudaerrorcapturedevent",
+                  "operation not permitted on an event last recorded in a capturing stream",
+                  "capture was invalidated", "capture sequence", "stream capture")
+
+
 def _is_capture_error(e):
     """Does this exception say that stream capture was refused (rather than that a call was wrong)?  HIP's
-    stream-capture error codes are 900-908 (hipErrorStreamCapture*, hipErrorCapturedEvent); torch and RCCL name
-    the capture in their messages.  The C ABI's FEA_EINVAL ('invalid arguments') is never one."""
+    stream-capture error codes 900-908 (hipErrorStreamCapture*, hipErrorCapturedEvent) by number or name, and the
+    wording torch and RCCL use for a call made while a stream captures.  Nothing else: the C ABI's FEA_EINVAL
+    ('invalid arguments'), autograd's 'backward through the graph' or a fault during a graph replay propagate."""
     msg = str(e)
     if "invalid arguments" in msg:
         return False
-    if any(f"hipError_t {c})" in msg for c in range(900, 909)):
+    if any(f"hipError_t {c})" in msg or f"error {c}" in msg for c in range(900, 909)):
         return True
     low = msg.lower()
-    return "captur" in low or "graph" in low
+    return any(w in low for w in _CAPTURE_WORDS)
 
 
 def ctypes_addr(arr):
@@ -1116,12 +1137,13 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.gpu = dist.get_backend(group) == "nccl"
-        # DDSolver captures whole cycles (kernels + RCCL calls) in HIP graphs by default on RCCL (host issue 4-5 us
-        # per cycle instead of 42-52, no graph-launch gaps between segments); if any rank's capture is refused,
-        # all ranks fall back to one graph per kernel segment (DDSolver._vcycle_captured).  FEANET_DD_CAPTURE=0
-        # turns it off.
+        # Whole-cycle capture (kernels + RCCL calls in one HIP graph per block of cycles; host issue 4-5 us per cycle
+        # instead of 42-52) is OPT-IN (capture=True or FEANET_DD_CAPTURE=1): it has run against stand-in
+        # communicators only, never on a multi-rank RCCL job, so the default is the segment-wise path (one graph per
+        # kernel segment between communication steps).  bench.py times both on every N > 1 line (dd_modes) under a
+        # bounded phase.  If any rank's capture is refused, all ranks fall back together (_vcycle_captured).
         self.capturable = self.gpu and capture if capture is not None else (
-            self.gpu and os.environ.get("FEANET_DD_CAPTURE", "1") != "0")
+            self.gpu and os.environ.get("FEANET_DD_CAPTURE", "0") == "1")
 
     def exchange(self, s, l, name, d):
         self.exchange_many(s, [(l, name, d)])

@@ -116,6 +116,37 @@ def test_c4_agglomeration_level_is_the_measured_best(P):
     assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == (4 if P >= 8 else 5)
 
 
+@pytest.mark.parametrize("m,n,P,Pc,want", [(4096, 4096, 2, 1, 4), (4096, 4096, 4, 2, 4), (4096, 4096, 8, 2, 3),
+                                            (16384, 16384, 8, 2, 5), (2048, 2048, 2, 1, 3), (8192, 4096, 4, 1, 4)])
+def test_default_agglomeration_other_sizes(m, n, P, Pc, want):
+    """The agglomeration rule off the one grid it was measured on (8193^2): the first level whose global grid has
+    <= 2^18 nodes below 8 ranks, <= 2^20 from 8 on, capped by what the partition can still split.  These pins fix the
+    rule's behaviour at other sizes; they are not measured optima (no communication is modelled)."""
+    Pr = P // Pc
+    Ld = default_agglomeration(m, n, Pr, global_levels(m, n), Pc=Pc)
+    assert Ld == want
+    cap = (1 << 20) if P >= 8 else (1 << 18)
+    Partition(m, n, Pr, Ld)
+    assert ((m >> Ld) + 1) * ((n >> Ld) + 1) <= cap or m // (Pr << (Ld + 1)) < 4 or m % (Pr << (Ld + 1))
+
+
+@pytest.mark.parametrize("msg,want", [
+    ("operation not permitted when stream is capturing", True),
+    ("HIP error: hipErrorStreamCaptureUnsupported (hipError_t 900)", True),
+    ("CUDA error: operation failed due to a previous error during capture: hipErrorStreamCaptureInvalidated", True),
+    ("NCCL error: stream is capturing", True),
+    ("Trying to backward through the graph a second time", False),
+    ("graph replay failed: an illegal memory access was encountered", False),
+    ("feanet_amd: fea_dd_copy_blocks failed (invalid arguments) while capturing", False),
+    ("NCCL communicator was aborted on rank 3", False),
+])
+def test_capture_error_classifier(msg, want):
+    """Only stream-capture refusals switch the decomposed solver to the segment-wise path; any other error —
+    including ones whose text mentions a graph — must propagate (dd._is_capture_error)."""
+    from feanet_amd.dd import _is_capture_error
+    assert _is_capture_error(RuntimeError(msg)) is want
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
