@@ -324,12 +324,14 @@ def test_dd_captured_cycles_match_segments(P, grid, rank, n):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
-@pytest.mark.parametrize("refuse", ["self", "peer", "einval"])
+@pytest.mark.parametrize("refuse", ["self", "peer", "einval", "peer_error"])
 def test_dd_capture_refusal_is_collective(refuse):
     """The captured path's fallback (DDSolver._vcycle_captured): a capture refused on this rank ('self': the
     communicator raises a stream-capture error inside the capture) or on another rank ('peer': this rank
     captures, the agreement all-reduce reports one refusal) drops EVERY rank to the segment-wise path, with the
-    cycles' results bitwise those of that path; an error that is not a capture refusal ('einval') propagates."""
+    cycles' results bitwise those of that path.  An error that is not a capture refusal is raised on every rank
+    after the same agreement all-reduce: the failing rank its own ('einval'), a rank whose peer failed a
+    RuntimeError naming it ('peer_error'), so no rank waits in a collective its peer never enters."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from tools.dd_projection import PackComm
@@ -350,8 +352,9 @@ def test_dd_capture_refusal_is_collective(refuse):
                     raise RuntimeError("feanet_amd: fea_dd_copy_blocks failed (invalid arguments)")
             return super().exchange_many(s, items, wait, packed)
 
-        def allreduce_sum(self, t):
-            return t + 1 if refuse == "peer" else t
+        def allreduce_sum(self, t):  # [refusals, other errors] of this rank plus one peer's
+            peer = {"peer": [1.0, 0.0], "peer_error": [0.0, 1.0]}.get(refuse, [0.0, 0.0])
+            return t + torch.tensor(peer, dtype=t.dtype, device=t.device)
 
     outs = []
     for comm in (PackComm(), Refusing()):
@@ -359,9 +362,9 @@ def test_dd_capture_refusal_is_collective(refuse):
         s = DDSolver(n, n, rank, P, comm=comm, agglomerate=2, grid=grid)
         s.set_rhs(f)
         s.load()
-        if refuse == "einval" and comm.capturable:
+        if refuse in ("einval", "peer_error") and comm.capturable:
             s.vcycle(3)  # eager once
-            with pytest.raises(RuntimeError, match="invalid arguments"):
+            with pytest.raises(RuntimeError, match="invalid arguments" if refuse == "einval" else "peer rank"):
                 s.vcycle(3)
             return
         for k in (1, 3, 3, 3, 2):
