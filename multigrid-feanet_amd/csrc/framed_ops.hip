@@ -2859,10 +2859,10 @@ static int num_cus() {
 // independent of the task height.  Same-process A/B against the power-of-two height
 // (profiles/r03_stream/balance_ab.txt): join -13.5 % at 4097^2, -3 % at 8193^2, -6 % on C3, -11 % at 2049^2
 // fp32; sweep+restriction -2 .. -12 %.  Batches of many samples are the exception (cycle_join_rb).
-static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2) {
+static int balanced_rb(int B, int nstrips, int rows_c, int halo, int rb_pow2, int min_waves = kTargetWaves) {
   if (rows_c < 2) return rb_pow2;
   const long long ncu = num_cus();
-  const long long min_wg = std::max<long long>(1, target_waves() / kWaves);
+  const long long min_wg = std::max<long long>(1, min_waves / kWaves);
   long long best_cost = -1;
   int best = rb_pow2;
   for (int rbc = 1; rbc <= rows_c && 2 * rbc <= 4 * rb_pow2; ++rbc) {
@@ -2975,11 +2975,15 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
 // than few long balanced ones there (256 x 1025^2 fp32 join 899 -> 843 us, 16 x 1025^2 59.4 -> 57.3 us;
 // 8 x 2049^2 fp64 prefers balanced, 201 vs 207 us; profiles/r03_stream/balance_ab.txt).
 constexpr int kJoinBatchPow2 = 16;
+#ifndef FEA_JOIN_MINW
+#define FEA_JOIN_MINW 1536
+#endif
+constexpr int kJoinMinWaves = FEA_JOIN_MINW;  // the fewest waves a cycle-join launch may have
 template <typename T>
 static void join_config(int B, int H, int W, MgArgs<T>& g) {
   g.nstrips = div_up(W - 2, Ovl3<T>::S);
   const int rb_pow2 = pick_rb(B, g.nstrips, H - 2, join_max_rb());
-  g.rb = B >= kJoinBatchPow2 ? rb_pow2 : balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, rb_pow2);
+  g.rb = B >= kJoinBatchPow2 ? rb_pow2 : balanced_rb(B, g.nstrips, (H + 1) / 2 - 2, 7, rb_pow2, kJoinMinWaves);
 #ifdef FEA_LAB_JOIN_RB  // lab builds: a fixed task height (fine rows, even) for A/B runs
   g.rb = FEA_LAB_JOIN_RB;
 #endif
@@ -3347,6 +3351,9 @@ constexpr int kZr2Waves = FEA_ZR2_WAVES;
 #ifndef FEA_BAL2
 #define FEA_BAL2 1
 #endif
+#ifndef FEA_BAL2_WAVES  // the fewest waves a two-level launch may have (lab builds vary it)
+#define FEA_BAL2_WAVES 1024
+#endif
 static int balanced_units(int B, int nstrips, int rows_u, int k, int ovh, int fallback, int umax = 256) {
 #if FEA_BAL2
   const long long ncu = num_cus();
@@ -3354,7 +3361,7 @@ static int balanced_units(int B, int nstrips, int rows_u, int k, int ovh, int fa
   int bu = fallback;
   for (int u = 1; u <= rows_u && u <= umax && k * u <= 256; ++u) {
     const long long ntr = div_up(rows_u, u), waves = (long long)B * nstrips * ntr;
-    if (waves < 2048) break;
+    if (waves < FEA_BAL2_WAVES) break;
     const long long wgs = (long long)B * div_up(ntr * nstrips, kWaves);
     const long long cost = div_up(wgs, ncu) * (k * u + ovh);
     if (best < 0 || cost < best) best = cost, bu = u;

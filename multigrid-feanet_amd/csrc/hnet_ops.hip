@@ -187,63 +187,75 @@ struct HSArgs {
 //   hold the iterate's values there, as in the buffer the separate kernels would read), the residual f - K out of
 //   the middle row is formed one row later and three residual rows close a coarse row (k_mg_resid_restrict's
 //   expressions); the wave loads two more halo columns per side and a task owns rb/2 coarse rows.
-template <typename T, bool MULTI, bool ZERO, bool RAW, int NL, int MODE>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1))) void k_mg_hsweep_strip(HSArgs<T> g) {
-  static_assert(MODE != 1 || !ZERO, "the prolongation variant corrects a stored iterate");
-  constexpr int V = HVec<T>::V;
-  constexpr int Q = V / 2;
-  constexpr int HALO = NL + 1;                 // columns / rows the stage chain reaches on each side
+// geometry of a wave's task (shared by the kernel's interior test and the task body)
+template <typename T, int NL, int MODE>
+struct HSGeo {
+  static constexpr int V = HVec<T>::V;
+  static constexpr int HALO = NL + 1;  // columns / rows the stage chain reaches on each side
   // MODE 1: the corrected iterate is wrong on the leftmost loaded column too (its left coarse node comes from a
   // lane the wave does not have); MODE 2: the residual and the restriction reach one column each further
-  constexpr int HALOC = HALO + (MODE == 2 ? 2 : MODE == 1 ? 1 : 0);
-  constexpr int HLN = (HALOC + V - 1) / V;     // halo lanes per side
-  constexpr int S = (64 - 2 * HLN) * V;        // owned columns per strip
-  constexpr int OFF = 128 / (int)sizeof(T) - 1;
-  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kHTS : 1];
-  __shared__ T tb2[(MULTI && MODE != 0) ? FEA_MAX_PATTERNS * kHTS : 1];  // P (MODE 1) or R (MODE 2) kernels
-  if constexpr (MULTI) {
-    for (int i = threadIdx.x; i < g.ntab * kHTS; i += 256) {
-      const int p = i / kHTS, d = i - p * kHTS;
-      tab[i] = d == 9 ? g.omd[p] : g.ktab[p * 9 + d];
-      if constexpr (MODE != 0) tb2[i] = d == 9 ? T(0) : (MODE == 1 ? g.ptab : g.rtab)[p * 9 + d];
-    }
-    __syncthreads();
+  static constexpr int HALOC = HALO + (MODE == 2 ? 2 : MODE == 1 ? 1 : 0);
+  static constexpr int HLN = (HALOC + V - 1) / V;  // halo lanes per side
+  static constexpr int S = (64 - 2 * HLN) * V;     // owned columns per strip
+};
+
+// out rows owned [r0, r1) and computed [rc0, rc1) of row task t (MODE 2: coarse rows [I0, I1))
+template <int MODE>
+__device__ __forceinline__ void hs_rows(int t, int rb, int H, int Hc, int& r0, int& r1, int& rc0, int& rc1, int& I0,
+                                        int& I1) {
+  I0 = I1 = 0;
+  if constexpr (MODE == 2) {
+    I0 = 1 + t * (rb / 2);
+    I1 = min(I0 + rb / 2, Hc - 1);
+    r0 = 2 * I0 - 1;
+    r1 = I1 == Hc - 1 ? H - 1 : 2 * I1 - 1;
+    rc0 = 2 * I0 - 2;
+    rc1 = 2 * I1 + 1;
+  } else {
+    r0 = 1 + t * rb;
+    r1 = min(r0 + rb, H - 1);
+    rc0 = r0;
+    rc1 = r1;
   }
-  // (row task, strip) pairs of one sample in linear order, four per workgroup
-  const int per = g.ntr * g.nstrips;
-  const int wpb = (per + 3) / 4;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = bid / wpb;
-  const int w = (bid - b * wpb) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (w >= per) return;
-  const int t = w / g.nstrips, s = w - t * g.nstrips;
+}
+
+// FEA_HS_INNER (lab): a wave whose task lies inside the grid with its whole reach (every row it streams, every column
+// its lanes load, every coarse row it reads) runs the EDGE = false body: no boundary / edge selects (j - u, the masked
+// HNet stages, the prolonged correction, the out row's stand-in values), no row or lane clamps, no partial stores,
+// no loads of the iterate's boundary values.  Same per-node expressions: bitwise the general body (GPU hnet tests
+// pass with it).  Measured slower, so off: the interior body has 19 % fewer VALU per step (800 vs 990 per 6-step
+// loop of the fp64 sweep + restriction, same 231 VGPRs) yet the 4097^2 MG-HJac cycle ran 411 instead of 396 us
+// (fea_mg_hsweep_restrict 123 vs 111 us, same lease, three alternations; profiles/r06_ab/hjac_inner_rejected.txt):
+// the kernel then carries both bodies (7186 instead of 4290 instructions) and waves of both kinds share each CU's
+// instruction cache.
+#ifndef FEA_HS_INNER
+#define FEA_HS_INNER 0
+#endif
+
+// One (row task, strip) of the streaming sweep (see k_mg_hsweep_strip).
+template <typename T, bool MULTI, bool ZERO, bool RAW, int NL, int MODE, bool EDGE>
+__device__ __forceinline__ void hsweep_task(const HSArgs<T>& g, int b, int t, int s, const T* tab, const T* tb2) {
+  static_assert(MODE != 1 || !ZERO, "the prolongation variant corrects a stored iterate");
+  using G = HSGeo<T, NL, MODE>;
+  constexpr int V = HVec<T>::V;
+  constexpr int Q = V / 2;
+  constexpr int HALO = G::HALO;
+  constexpr int HLN = G::HLN;
+  constexpr int S = G::S;
+  constexpr int OFF = 128 / (int)sizeof(T) - 1;
   const int lane = lane_id();
   const int H = g.H, W = g.W, ld = g.ld;
   const int cs = 1 + s * S - HLN * V;  // first loaded column
   const int cl = cs + V * lane;
-  const int ll = min(lane, (W - 1 - cs) / V);  // lanes past the last column re-read a valid line
+  const int ll = EDGE ? min(lane, (W - 1 - cs) / V) : lane;  // lanes past the last column re-read a valid line
   const bool own = lane >= HLN && lane < 64 - HLN;
-  // out rows owned [r0, r1) and computed [rc0, rc1)
-  int r0, r1, rc0, rc1, I0 = 0, I1 = 0;
-  if constexpr (MODE == 2) {
-    I0 = 1 + t * (g.rb / 2);
-    I1 = min(I0 + g.rb / 2, g.Hc - 1);
-    r0 = 2 * I0 - 1;
-    r1 = I1 == g.Hc - 1 ? H - 1 : 2 * I1 - 1;
-    rc0 = 2 * I0 - 2;
-    rc1 = 2 * I1 + 1;
-  } else {
-    r0 = 1 + t * g.rb;
-    r1 = min(r0 + g.rb, H - 1);
-    rc0 = r0;
-    rc1 = r1;
-  }
+  int r0, r1, rc0, rc1, I0, I1;
+  hs_rows<MODE>(t, g.rb, H, g.Hc, r0, r1, rc0, rc1, I0, I1);
   bool cin[V], cgr[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    cin[k] = cl + k >= 1 && cl + k <= W - 2;
-    cgr[k] = cl + k >= 0 && cl + k <= W - 1;
+    cin[k] = !EDGE || (cl + k >= 1 && cl + k <= W - 2);
+    cgr[k] = !EDGE || (cl + k >= 0 && cl + k <= W - 1);
   }
   T ks[9], om = 0, hk[NL > 0 ? NL : 1][9], t2[9];
   if constexpr (!MULTI) {
@@ -264,11 +276,14 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   const T* __restrict__ fb = g.f + boff;
   T* __restrict__ ob = g.out + boff;
   const uint8_t* __restrict__ pb = MULTI ? g.pid + OFF + cs : nullptr;
-  auto rowo = [&](int r) -> long long { return (long long)(min(max(r, -1), H) + 1) * ld + V * ll; };
+  auto rowo = [&](int r) -> long long {
+    if constexpr (EDGE) r = min(max(r, -1), H);
+    return (long long)(r + 1) * ld + V * ll;
+  };
 
   // MODE 1: the lane's coarse values (cl + 1) / 2 + q, q < Q, and the left lane's last one (DPP)
   const int jc = (cs + 1) / 2;
-  const int llc = MODE == 1 ? min(lane, (g.Wc - 1 - jc) / Q) : 0;
+  const int llc = MODE == 1 ? (EDGE ? min(lane, (g.Wc - 1 - jc) / Q) : lane) : 0;
   const T* __restrict__ eb = MODE == 1 ? g.ec + (long long)b * g.bsc + OFF + jc + Q * llc : nullptr;
   const uint8_t* __restrict__ pcb = (MODE == 1 && MULTI) ? g.pidc + OFF + jc + Q * llc : nullptr;
   struct CR {  // coarse row: e[0] = column (cl-1)/2 (left lane), e[1..Q] = own; pattern offsets o[]
@@ -281,7 +296,8 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   };
   auto crow_ld = [&](int a) {
     CRaw r;
-    const long long o = (long long)(min(max(a, -1), g.Hc) + 1) * g.ldc;
+    if constexpr (EDGE) a = min(max(a, -1), g.Hc);
+    const long long o = (long long)(a + 1) * g.ldc;
     if constexpr (MODE == 1) {
       if constexpr (Q == 1) {
         r.x[0] = eb[o];
@@ -347,7 +363,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   T ur[PF][V], fr_[PF][V], rw_[PF][V], frr[PF][V], uo[PF][V];
   int pr[PF][V], po[PF][V];
   // MODE 2 needs the iterate's values of an out row only where they stand in for the sweep (boundary nodes)
-  auto need_uo = [&](int yy) { return !(yy >= 1 && yy <= H - 2) || !cin[0] || !cin[V - 1]; };
+  auto need_uo = [&](int yy) { return EDGE && (!(yy >= 1 && yy <= H - 2) || !cin[0] || !cin[V - 1]); };
   auto fill = [&](int sl, int y) {
 #pragma unroll
     for (int k = 0; k < V; ++k) ur[sl][k] = T(0);
@@ -358,7 +374,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     if constexpr (MODE == 2) {
       hload<T, V>(fb + rowo(y - 2 - NL), frr[sl]);
       if constexpr (MULTI) hpload<V>(pb + rowo(y - 1 - NL), po[sl]);
-      if constexpr (!ZERO) {
+      if constexpr (!ZERO && EDGE) {
 #pragma unroll
         for (int k = 0; k < V; ++k) uo[sl][k] = T(0);
         if (need_uo(y - 1 - NL)) hload<T, V>(ub + rowo(y - 1 - NL), uo[sl]);
@@ -379,7 +395,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   auto step = [&](int y, auto pos_c) __attribute__((always_inline)) {
     constexpr int SL = decltype(pos_c)::value % PF;
     constexpr bool ODD = decltype(pos_c)::value & 1;  // y odd (y0 is even)
-    int z = y & g.zmask;  // 0 at run time, unknown to the compiler: the weight loads stay in the step
+    int z = __builtin_amdgcn_readfirstlane(y & g.zmask);  // 0 at run time, unknown to the compiler: the weight loads stay in the step
     // stage barrier: z is "changed" by an empty asm, so the weight loads after it cannot be hoisted above it —
     // each stage's weights are loaded just before the stage and die after it (one stage's worth of SGPRs live).
     // fp64 only: 4097^2 MG-HJac 486 -> 456 us (prolongation+sweep 101.6 -> 96.7 us, level 1 38.3 -> 30.5 us);
@@ -414,14 +430,14 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
       py[k] = MULTI ? pr[SL][k] : 0;
       raw[k] = RAW ? rw_[SL][k] : T(0);
       fres[k] = MODE == 2 ? frr[SL][k] : T(0);
-      uout[k] = (MODE == 2 && !ZERO) ? uo[SL][k] : T(0);
+      uout[k] = (MODE == 2 && !ZERO && EDGE) ? uo[SL][k] : T(0);
       pout[k] = (MODE == 2 && MULTI) ? po[SL][k] : 0;
     }
     fill(SL, y + PF);  // (rows past the task's last are clamped into the frame: loaded, never used)
     if constexpr (MODE == 1) {
       stage_t2();
       // x(y) = u(y) + w1 P(ec) on the interior (correct_even / correct_odd of k_mg_prolong)
-      const bool yin = y >= 1 && y <= H - 2;
+      const bool yin = !EDGE || (y >= 1 && y <= H - 2);
 #pragma unroll
       for (int k = 0; k < V; ++k) {  // (branch-free: a select, not a divergent branch per column)
         T xk;
@@ -450,7 +466,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     // j and d_0 of row y-1
     stage_ks();
     const int yj = y - 1;
-    const bool rin = yj >= 1 && yj <= H - 2, rgr = yj >= 0 && yj <= H - 1;
+    const bool rin = !EDGE || (yj >= 1 && yj <= H - 2), rgr = !EDGE || (yj >= 0 && yj <= H - 1);
     T d0[V], jv[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -510,7 +526,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     for (int l = 1; l <= NL; ++l) {
       stage_hk(l - 1);
       const int yl = y - 1 - l;
-      const bool lin = yl >= 1 && yl <= H - 2;
+      const bool lin = !EDGE || (yl >= 1 && yl <= H - 2);
       T dl[V];
 #pragma unroll
       for (int k = 0; k < V; ++k) {
@@ -540,7 +556,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
     if (own && yo >= r0 && yo < r1) hstore<T, V>(ob + (long long)(yo + 1) * ld + V * lane, o, cin);
     if constexpr (MODE == 2) {
       // the out row as the buffer would hold it: the iterate's own values off the interior
-      const bool oin = yo >= 1 && yo <= H - 2;
+      const bool oin = !EDGE || (yo >= 1 && yo <= H - 2);
 #pragma unroll
       for (int k = 0; k < V; ++k) o[k] = (oin && cin[k]) ? o[k] : uout[k];
       O0 = O1;
@@ -624,7 +640,7 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
               T* cp = g.fc + (long long)b * g.bsc + OFF + (long long)(I + 1) * g.ldc + Jl;
 #pragma unroll
               for (int q = 0; q < Q; ++q)
-                if (Jl + q <= g.Wc - 2) cp[q] = oc[q];
+                if (!EDGE || Jl + q <= g.Wc - 2) cp[q] = oc[q];
             }
           }
 #pragma unroll
@@ -642,6 +658,46 @@ __attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1)
   hs_unroll<U - 1>([&](auto i) __attribute__((always_inline)) {
     if (y + decltype(i)::value <= y1) step(y + decltype(i)::value, i);
   });
+}
+
+template <typename T, bool MULTI, bool ZERO, bool RAW, int NL, int MODE>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(hs_mode1_wide<T, MULTI, MODE, RAW>() ? 3 : 1))) void k_mg_hsweep_strip(HSArgs<T> g) {
+  using G = HSGeo<T, NL, MODE>;
+  constexpr int V = HVec<T>::V;
+  __shared__ T tab[MULTI ? FEA_MAX_PATTERNS * kHTS : 1];
+  __shared__ T tb2[(MULTI && MODE != 0) ? FEA_MAX_PATTERNS * kHTS : 1];  // P (MODE 1) or R (MODE 2) kernels
+  if constexpr (MULTI) {
+    for (int i = threadIdx.x; i < g.ntab * kHTS; i += 256) {
+      const int p = i / kHTS, d = i - p * kHTS;
+      tab[i] = d == 9 ? g.omd[p] : g.ktab[p * 9 + d];
+      if constexpr (MODE != 0) tb2[i] = d == 9 ? T(0) : (MODE == 1 ? g.ptab : g.rtab)[p * 9 + d];
+    }
+    __syncthreads();
+  }
+  // (row task, strip) pairs of one sample in linear order, four per workgroup
+  const int per = g.ntr * g.nstrips;
+  const int wpb = (per + 3) / 4;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bid / wpb;
+  const int w = (bid - b * wpb) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w >= per) return;
+  const int t = w / g.nstrips, s = w - t * g.nstrips;
+  if constexpr (FEA_HS_INNER != 0) {
+    // interior: the rows streamed (from the first fill step 2 + NL rows above the first computed one, through the
+    // prefetch past the last), the loaded columns and (MODE 1) the coarse rows read all lie strictly inside the grid
+    int r0, r1, rc0, rc1, I0, I1;
+    hs_rows<MODE>(t, g.rb, g.H, g.Hc, r0, r1, rc0, rc1, I0, I1);
+    const int cs = 1 + s * G::S - G::HLN * V;
+    const int ya = ((rc0 - G::HALO) & ~1) - 3 - NL, yz = rc1 + G::HALO + 4;
+    const bool inner = cs >= 1 && cs + 64 * V - 1 <= g.W - 2 && ya >= 1 && yz <= g.H - 2 &&
+                       (MODE != 1 || ((ya >> 1) - 1 >= 1 && (yz >> 1) + 4 <= g.Hc - 2));
+    if (__builtin_amdgcn_readfirstlane((int)inner)) {  // wave-uniform (scalar branch)
+      hsweep_task<T, MULTI, ZERO, RAW, NL, MODE, false>(g, b, t, s, tab, tb2);
+      return;
+    }
+  }
+  hsweep_task<T, MULTI, ZERO, RAW, NL, MODE, true>(g, b, t, s, tab, tb2);
 }
 
 }  // namespace fea
@@ -704,6 +760,9 @@ static int hs_num_cus() {
 // the CUs ran a third task).  Levels too small for 2048 waves at any height take the cheapest height outright:
 // there every CU holds at most one or two tasks and the task's chain of rows is the time.  Results are bitwise
 // independent of the task height.
+#ifndef FEA_HS_MINW  // the fewest waves a balanced hsweep launch may have (lab builds vary it)
+#define FEA_HS_MINW 2048
+#endif
 static int hs_units_per_task(int B, int nstrips, int rows_u, int k, int ovh) {
 #if FEA_HSWEEP_BALANCED
   const long long ncu = hs_num_cus();
@@ -713,7 +772,7 @@ static int hs_units_per_task(int B, int nstrips, int rows_u, int k, int ovh) {
     const long long ntr = (rows_u + u - 1) / u, waves = (long long)B * nstrips * ntr;
     const long long wgs = (long long)B * ((ntr * nstrips + 3) / 4);
     const long long cost = ((wgs + ncu - 1) / ncu) * (k * u + ovh);
-    if (waves >= 2048 && (best_ok < 0 || cost < best_ok)) best_ok = cost, u_ok = u;
+    if (waves >= FEA_HS_MINW && (best_ok < 0 || cost < best_ok)) best_ok = cost, u_ok = u;
     if (best_any < 0 || cost < best_any) best_any = cost, u_any = u;
   }
   return best_ok >= 0 ? u_ok : u_any;
