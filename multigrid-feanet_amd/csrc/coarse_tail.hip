@@ -89,6 +89,11 @@ __device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element off
 // ---------------------------------------------------------------------------------------------
 constexpr int kTailDownRows = 2;  // coarse rows per wave going down: Hc - 2 <= 31 over 16 waves
 constexpr int kTailUpRows = 4;    // fine rows per wave going up / at the coarsest level: H - 2 <= 63
+// FEA_TAIL_LATE_SYNC: the two-material 65^2 tail takes its staging barrier inside the first phase (down_rows SYNC)
+#ifndef FEA_TAIL_LATE_SYNC
+#define FEA_TAIL_LATE_SYNC 1
+#endif
+constexpr bool kTailLateSync = FEA_TAIL_LATE_SYNC != 0;
 
 // HT != 0: the grid is HT x HT with NLEV levels, known at compile time (every BASELINE configuration
 // ends in the 65^2 .. 3^2 tail), so level sizes, offsets and rows per wave fold into immediates.
@@ -178,7 +183,11 @@ struct TailFast {
   // level k (offset o) -> f_{k+1}; PER coarse rows per wave.  GLOBAL: f_k is f_t in HBM (level 0);
   // the wave then also writes the rows it loaded into LDS for the up phase (overlapping rows of
   // neighbouring waves are written twice with the same value), which replaces a separate staging pass.
-  template <bool GLOBAL, int PER>
+  // SYNC (the first phase of a two-material FIX65 tail): the workgroup barrier that makes the staged tables and
+  // pattern maps visible is taken here, after this phase's f_t rows were requested from HBM, so the two memory
+  // round trips overlap instead of following each other (every wave has rows in that phase: 31 coarse rows over
+  // 16 waves).
+  template <bool GLOBAL, int PER, bool SYNC = false>
   __device__ __forceinline__ void down_rows(int k, int o, int I0, int I1) const {
     constexpr int R = 2 * PER + 3;
     const int H = Hk(k), N = Nk(k), Hc = (H + 1) / 2, Nc = (N + 1) / 2;
@@ -193,8 +202,10 @@ struct TailFast {
       const int y = min(yb + j, H - 1);
       if constexpr (GLOBAL) fr[j] = fg[(long long)y * ld + lane];
       else fr[j] = f[y * N + lane];
-      q[j] = pat(pk, H, N, yb + j);
     }
+    if constexpr (SYNC) __syncthreads();
+#pragma unroll
+    for (int j = 0; j < R; ++j) q[j] = pat(pk, H, N, yb + j);
     if constexpr (GLOBAL) {
 #pragma unroll
       for (int j = 0; j < R; ++j)
@@ -234,6 +245,10 @@ struct TailFast {
     const int Hc = (Hk(k) + 1) / 2;
     const int per = (Hc - 2 + kWaves - 1) / kWaves;  // <= kTailDownRows
     const int I0 = 1 + wv * per, I1 = min(Hc - 1, I0 + per);
+    if constexpr (GLOBAL && MULTI && HT == 65 && kTailLateSync) {  // 31 coarse rows: every wave has two
+      down_rows<true, kTailDownRows, true>(k, o, I0, I1);
+      return;
+    }
     if (I0 >= I1) return;  // wave-uniform
     if (per == 1) down_rows<GLOBAL, 1>(k, o, I0, I1);
     else down_rows<GLOBAL, kTailDownRows>(k, o, I0, I1);
@@ -491,7 +506,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
   if constexpr (FIX65) {
     // the first down phase reads f_t from HBM itself and stages it for the up phase; single pattern:
     // the tables come from uniform loads, so nothing has to land before it
-    if (MULTI) FEA_TAIL_SYNC();
+    if (MULTI && !kTailLateSync) FEA_TAIL_SYNC();  // (else the first phase takes it after its HBM loads)
     tail_fast<T, MULTI, 65, 6>(a, va, fs, ktb, rtb, ptb, pl, wv, lane
 #ifdef FEA_TAIL_TRACE
                                , nph

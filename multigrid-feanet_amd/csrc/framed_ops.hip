@@ -2975,10 +2975,14 @@ extern "C" size_t fea_norm_workspace_bytes(int B, int H, int W) {
 // than few long balanced ones there (256 x 1025^2 fp32 join 899 -> 843 us, 16 x 1025^2 59.4 -> 57.3 us;
 // 8 x 2049^2 fp64 prefers balanced, 201 vs 207 us; profiles/r03_stream/balance_ab.txt).
 constexpr int kJoinBatchPow2 = 16;
+// The fewest waves a cycle-join launch may have: 1536 (the balance rule then picks 20-row tasks on 2049^2, 1854
+// waves: C3 join 40.5 -> 32.0 us, the 2049^2 Poisson join 24.6 -> 21.9 us; 4097^2 72-row tasks, 1995 waves: 79.1 ->
+// 77.1 us).  The two-material fp64 join runs two waves per SIMD (230 VGPRs), 2048 wave slots: its old 2646-wave
+// launch needed a second round on most CUs.  Same-lease A/B, profiles/r06_ab/join_minw.txt.
 #ifndef FEA_JOIN_MINW
 #define FEA_JOIN_MINW 1536
 #endif
-constexpr int kJoinMinWaves = FEA_JOIN_MINW;  // the fewest waves a cycle-join launch may have
+constexpr int kJoinMinWaves = FEA_JOIN_MINW;
 template <typename T>
 static void join_config(int B, int H, int W, MgArgs<T>& g) {
   g.nstrips = div_up(W - 2, Ovl3<T>::S);
@@ -3351,7 +3355,9 @@ constexpr int kZr2Waves = FEA_ZR2_WAVES;
 #ifndef FEA_BAL2
 #define FEA_BAL2 1
 #endif
-#ifndef FEA_BAL2_WAVES  // the fewest waves a two-level launch may have (lab builds vary it)
+// the fewest waves a two-level launch may have: 1024 (metric V-cycle 132.5 -> 131.0 us against 2048 — fewer,
+// taller tasks re-stream fewer overlap rows; 3072 / 4096 measured +4 us, 512 / 768 +1.5 us; profiles/r06_ab)
+#ifndef FEA_BAL2_WAVES
 #define FEA_BAL2_WAVES 1024
 #endif
 static int balanced_units(int B, int nstrips, int rows_u, int k, int ovh, int fallback, int umax = 256) {

@@ -757,11 +757,13 @@ static int hs_num_cus() {
 // balanced_rb): the slowest CU runs ceil(workgroups / CUs) tasks back to back, so the cost of a task height is
 // that count times the rows a task streams; among the heights that keep >= 2048 waves in flight the cheapest
 // wins (4097^2 fp64 sweep+restriction: 504 workgroups of 74 rows, 2 per CU, instead of 576 of 64: a quarter of
-// the CUs ran a third task).  Levels too small for 2048 waves at any height take the cheapest height outright:
+// the CUs ran a third task; "2048" is FEA_HS_MINW, now 1536).  Levels too small for 2048 waves at any height take the cheapest height outright:
 // there every CU holds at most one or two tasks and the task's chain of rows is the time.  Results are bitwise
 // independent of the task height.
-#ifndef FEA_HS_MINW  // the fewest waves a balanced hsweep launch may have (lab builds vary it)
-#define FEA_HS_MINW 2048
+// the fewest waves a balanced hsweep launch may have: 1536 (4097^2 MG-HJac 397.4 -> 393.3 us, fine sweep +
+// restriction 111 -> 109 us, against 2048; 1024 measured the same as 1536; profiles/r06_ab/hjac_minw.txt)
+#ifndef FEA_HS_MINW
+#define FEA_HS_MINW 1536
 #endif
 static int hs_units_per_task(int B, int nstrips, int rows_u, int k, int ovh) {
 #if FEA_HSWEEP_BALANCED

@@ -52,18 +52,16 @@ def global_levels(m, n):
 
 
 def default_agglomeration(m, n, P, L, max_nodes=None, Pc=1):
-    """Smallest Ld whose global level has <= max_nodes nodes, within what the partition allows (P row
-    blocks, Pc column blocks).  Default max_nodes: 2^18 below 8 ranks, 2^20 from 8 on — at 8193^2 (BASELINE C4)
-    Ld = 5 (257^2) at 2 and 4 ranks, Ld = 4 (513^2) at 8: the per-rank projection with whole cycles captured (the
-    RCCL default) runs 267.0 / 160.7 us at Ld = 5 vs 285.6 / 167.5 at Ld = 4 on 2 / 4 ranks (the replicated coarse
-    sub-cycle is shorter, the doubled ghost frames of the small levels cost less), and 116.7 at Ld = 4 vs 119.2 at
-    Ld = 5 on 8, where the blocks are small enough that the doubled ghost frames cost more
-    (profiles/r05_dd/dd_projection.txt).  Scope of that evidence: ONE grid (8193^2) and single-GPU projections whose
-    communicator moves nothing, so message and all-gather costs are not modelled; for other grids the rule is
-    only "stop coarsening the distributed levels once the global level is this small", pinned by
-    tests/test_dd.py for several sizes, not a measured optimum."""
+    """Smallest Ld whose global level has <= max_nodes nodes (default 2^18), within what the partition allows (P
+    row blocks, Pc column blocks).  At 8193^2 (BASELINE C4) that is Ld = 5 (257^2) at 2, 4 and 8 ranks: the per-rank
+    projection (one rank's whole captured program on one GPU, tools/dd_projection.py, profiles/r06_dd) runs 257.2 /
+    156.6 / 109.1 us at Ld = 5 against 279.5 / 161.1 / 111.5 at Ld = 4 and 278.2 / 168.5 / 118.3 at Ld = 6 on 2 / 4 / 8
+    ranks (round 5, before the round-6 task heights, had Ld = 4 ahead at 8 ranks).  Scope of that evidence: ONE grid
+    and single-GPU projections whose communicator moves nothing, so message and all-gather costs are not modelled;
+    for other grids the rule is only "stop coarsening the distributed levels once the global level is this small",
+    pinned by tests/test_dd.py for several sizes, not a measured optimum."""
     if max_nodes is None:
-        max_nodes = (1 << 20) if P * Pc >= 8 else (1 << 18)
+        max_nodes = 1 << 18
     Ld = 1
     while Ld < L - 1 and ((m >> Ld) + 1) * ((n >> Ld) + 1) > max_nodes and m % (P << (Ld + 1)) == 0 \
             and m // (P << (Ld + 1)) >= 4 and n % (Pc << (Ld + 1)) == 0 and (Pc == 1 or n // (Pc << (Ld + 1)) >= 4):

@@ -103,29 +103,25 @@ def test_default_agglomeration():
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_c4_agglomeration_level_is_the_measured_best(P):
     """C4 (8193^2 over the bench's 2x1 / 2x2 / 4x2 blocks): the default agglomeration level is the one the
-    per-rank projection chose.  Round 3 (segment graphs): Ld = 4 (the 513^2 level), fastest at every rank count against Ld = 3, 5, 6
-    (tools/dd_projection.py, profiles/r03_dd/dd_projection.txt: 8 ranks 151.8 us vs 158.5 / 155.9 / 154.7), and
-    with the round-3 two-level launches within the run-to-run spread of Ld = 3 / 5 at 4 and 8 ranks
-    (profiles/r03_dd/dd_projection_paired.txt: 134.0 vs 135.8 / 135.7 us at 8 ranks).  Round 4 measured the
-    projection with whole cycles captured: Ld = 5 at 2 and 4 ranks 270.5 / 161.8 vs 287.9 / 170.3 us for Ld = 4,
-    level at 8 ranks (116.9 us both; profiles/r04_dd/dd_projection.txt).  Round 5 makes capture the RCCL default and
-    re-measured (profiles/r05_dd/dd_projection.txt): Ld = 5 at 2 / 4 ranks (267.0 / 160.7 vs 285.6 / 167.5 us), Ld = 4
-    at 8 (116.7 vs 119.2 us)."""
+    per-rank projection chose.  Round 6 (tools/dd_projection.py with the coarse sub-cycle timed as GPU graph replays,
+    profiles/r06_dd/dd_projection.txt): Ld = 5 (257^2) at 2 / 4 / 8 ranks, 257.2 / 156.6 / 109.1 us against 279.5 /
+    161.1 / 111.5 at Ld = 4 and 278.2 / 168.5 / 118.3 at Ld = 6.  (Rounds 3-5 measured Ld = 4 or 5 depending on the
+    rank count with the kernels of their time: profiles/r03_dd .. r05_dd.)"""
     from feanet_amd.dd import default_grid
     Pr, Pc = default_grid(P)
-    assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == (4 if P >= 8 else 5)
+    assert default_agglomeration(8192, 8192, Pr, global_levels(8192, 8192), Pc=Pc) == 5
 
 
-@pytest.mark.parametrize("m,n,P,Pc,want", [(4096, 4096, 2, 1, 4), (4096, 4096, 4, 2, 4), (4096, 4096, 8, 2, 3),
-                                            (16384, 16384, 8, 2, 5), (2048, 2048, 2, 1, 3), (8192, 4096, 4, 1, 4)])
+@pytest.mark.parametrize("m,n,P,Pc,want", [(4096, 4096, 2, 1, 4), (4096, 4096, 4, 2, 4), (4096, 4096, 8, 2, 4),
+                                            (16384, 16384, 8, 2, 6), (2048, 2048, 2, 1, 3), (8192, 4096, 4, 1, 4)])
 def test_default_agglomeration_other_sizes(m, n, P, Pc, want):
     """The agglomeration rule off the one grid it was measured on (8193^2): the first level whose global grid has
-    <= 2^18 nodes below 8 ranks, <= 2^20 from 8 on, capped by what the partition can still split.  These pins fix the
-    rule's behaviour at other sizes; they are not measured optima (no communication is modelled)."""
+    <= 2^18 nodes, capped by what the partition can still split.  These pins fix the rule's behaviour at other
+    sizes; they are not measured optima (no communication is modelled)."""
     Pr = P // Pc
     Ld = default_agglomeration(m, n, Pr, global_levels(m, n), Pc=Pc)
     assert Ld == want
-    cap = (1 << 20) if P >= 8 else (1 << 18)
+    cap = 1 << 18
     Partition(m, n, Pr, Ld)
     assert ((m >> Ld) + 1) * ((n >> Ld) + 1) <= cap or m // (Pr << (Ld + 1)) < 4 or m % (Pr << (Ld + 1))
 

@@ -6,3 +6,4 @@ timeout -k 10 300 python3 tools/dd_projection.py --ranks 2,4,8 --steps 50 --out 
 cat $T/dd_projection.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $T/dd_trace -o run -- python3 tools/dd_projection.py --ranks 8 --ld 4 --steps 50 > $T/dd_trace.log 2>&1 || { tail $T/dd_trace.log; exit 1; }
 python3 tools/trace_summary.py $T/dd_trace > $T/dd_trace_summary.txt && head -30 $T/dd_trace_summary.txt
+BENCH_ARGS="--n 2048 --problem interface --steps 300" REPS="1 2" bash tools/lab/gpu_cfg_libs.sh r06_ab3/c3 - lab_libs/tls0.so lab_libs/l1bal.so lab_libs/l1bal1024.so
