@@ -250,6 +250,31 @@ int fea_mg_zero_restrict2_f64(const double* f, double* fc, double* fc2, const ui
                               double w0, int B, int H, int W, int ld, long long bstride, int ldc,
                               long long bstridec, int ldc2, long long bstridec2, void* stream);
 
+/* Domain-decomposed agglomeration (feanet_amd/dd.py; the restriction is FEANet/multigrid.py:168-172):
+ * the zero-guess restrictions that produce the agglomerated level also store that level's block [r0, r1) x [c0, c1)
+ * (local rows / columns of the output level) into send[b][r - r0][c - c0] — the all-gather's send buffer — so no copy
+ * launch sits between the restriction and the all-gather.  Otherwise bitwise fea_mg_zero_restrict2 /
+ * fea_mg_residual_restrict(u = v_out = NULL).  Nodes of the block outside the output level's interior are not
+ * written (the caller keeps them zero). */
+int fea_mg_zero_restrict2_send_f32(const float* f, float* fc, float* fc2, const uint8_t* pid, const uint8_t* pidc,
+                                   const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab,
+                                   float w0, int B, int H, int W, int ld, long long bstride, int ldc,
+                                   long long bstridec, int ldc2, long long bstridec2, float* send, int r0, int r1,
+                                   int c0, int c1, void* stream);
+int fea_mg_zero_restrict2_send_f64(const double* f, double* fc, double* fc2, const uint8_t* pid, const uint8_t* pidc,
+                                   const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
+                                   double w0, int B, int H, int W, int ld, long long bstride, int ldc,
+                                   long long bstridec, int ldc2, long long bstridec2, double* send, int r0, int r1,
+                                   int c0, int c1, void* stream);
+int fea_mg_zero_restrict_send_f32(const float* f, float* fc, const uint8_t* pid, const float* ktab, const float* omd,
+                                  int ntab, const float* rtab, int nrtab, float w0, int B, int H, int W, int ld,
+                                  long long bstride, int ldc, long long bstridec, float* send, int r0, int r1, int c0,
+                                  int c1, void* stream);
+int fea_mg_zero_restrict_send_f64(const double* f, double* fc, const uint8_t* pid, const double* ktab,
+                                  const double* omd, int ntab, const double* rtab, int nrtab, double w0, int B, int H,
+                                  int W, int ld, long long bstride, int ldc, long long bstridec, double* send, int r0,
+                                  int r1, int c0, int c1, void* stream);
+
 /* Fused pre-smooth + residual + restriction on a level with a given iterate (temporal blocking):
  *   u_out = J(u, f) (interior)   and   fc(interior) = w0 * R(f - K u_out)
  * u and f are read once.  FEANet/multigrid.py:165 then :168-170 (MultiGrid.Step, mg_test :27352-27357).
@@ -444,6 +469,18 @@ int fea_mg_mid_down_f32(const float* const* f, const uint8_t* const* pid, int k,
 int fea_mg_mid_down_f64(const double* const* f, const uint8_t* const* pid, int k, int B, int H, int W,
                         const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab, double w0,
                         int TR, int TC, void* stream);
+/* mid_down of the agglomerated coarse problem of a domain-decomposed run (feanet_amd/dd.py): level a's f is read
+ * from the all-gather's buffer gsrc ([Pr * Pc][B][gcr][gcc], rank r's block of gcr x gcc nodes starting at
+ * node (1 + (r / Pc) gcr, 1 + (r % Pc) gcc); H - 1 = Pr gcr, W - 1 = Pc gcc) instead of f[0], and every tile also
+ * writes the interior nodes it owns into f[0] (framed) for the later launches — the placement copy of the
+ * gathered blocks folded into this launch.  Otherwise bitwise fea_mg_mid_down on the placed f[0]. */
+int fea_mg_mid_down_gathered_f32(const float* const* f, const uint8_t* const* pid, int k, int B, int H, int W,
+                                 const float* ktab, const float* omd, int ntab, const float* rtab, int nrtab, float w0,
+                                 int TR, int TC, const float* gsrc, int Pr, int Pc, int gcr, int gcc, void* stream);
+int fea_mg_mid_down_gathered_f64(const double* const* f, const uint8_t* const* pid, int k, int B, int H, int W,
+                                 const double* ktab, const double* omd, int ntab, const double* rtab, int nrtab,
+                                 double w0, int TR, int TC, const double* gsrc, int Pr, int Pc, int gcr, int gcc,
+                                 void* stream);
 int fea_mg_mid_up_f32(const float* const* f, const float* e, float* out, const uint8_t* const* pid, int k, int B,
                       int H, int W, const float* ktab, const float* omd, int ntab, const float* ptab, int nptab,
                       float w1, int TR, int TC, void* stream);

@@ -274,7 +274,19 @@ struct MgArgs {
   // rectangle by rectangle, rt[r] the first of rectangle r
   int nrect;
   int rI0[4], rI1[4], rc0[4], rc1[4], rns[4], rt[5];
+  // zero-guess restrictions of a domain-decomposed rank (k_mg_zero_restrict, k_mg_zero_restrict2): the output level's
+  // block [gr0, gr1) x [gc0, gc1) (local rows / columns) also goes to gsend[b][r - gr0][c - gc0] — the all-gather's
+  // send buffer of the agglomeration, written by the kernel that computes it instead of a copy launch after it
+  T* gsend;
+  int gr0, gr1, gc0, gc1;
 };
+
+// the agglomeration send-buffer store of a zero-guess restriction (MgArgs::gsend), node (r, c) of the output level
+template <typename T>
+__device__ __forceinline__ void gather_store(const MgArgs<T>& g, int b, int r, int c, T v) {
+  if (g.gsend && r >= g.gr0 && r < g.gr1 && c >= g.gc0 && c < g.gc1)
+    g.gsend[((long long)b * (g.gr1 - g.gr0) + (r - g.gr0)) * (g.gc1 - g.gc0) + (c - g.gc0)] = v;
+}
 
 struct TaskId {
   int b, s, t;
@@ -1066,6 +1078,11 @@ __global__ __launch_bounds__(256) void k_mg_zero_restrict(MgArgs<T> g) {
         for (int q = 0; q < Q; ++q)
           if (J0 + q <= Wc - 2) cp[q] = o[q];
       }
+      if (g.gsend) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (J0 + q <= Wc - 2) gather_store(g, id.b, I, J0 + q, o[q]);
+      }
     }
 #pragma unroll
     for (int k = 0; k <= V; ++k) Ra[k] = Rc[k];
@@ -1281,7 +1298,11 @@ __device__ __forceinline__ void zr2_task(const MgArgs<T>& g, const TaskId& id, c
             acc += tabv(rtb, p2.a[B0 + 1], 7) * r2.a[B0 + 1];
             acc += tabv(rtb, p2.a[B0 + 2], 8) * r2.a[B0 + 2];
           }
-          if (!(Jm & 1) && M >= Mlo && M < Mhi && M <= Wc2 - 2) cb2[(long long)(K + 1) * g.ldc2 + M] = w0 * acc;
+          if (!(Jm & 1) && M >= Mlo && M < Mhi && M <= Wc2 - 2) {
+            const T o2 = w0 * acc;
+            cb2[(long long)(K + 1) * g.ldc2 + M] = o2;
+            gather_store(g, id.b, K, M, o2);
+          }
         }
         Ro = R;
         if constexpr (MULTI) So = Qb;
@@ -3107,6 +3128,31 @@ extern "C" int fea_norm_append(const double* ws, long long stride, long long per
     }                                                                                                        \
     FEA_LAUNCH_CHECK();                                                                                      \
   }                                                                                                          \
+  extern "C" int fea_mg_zero_restrict_send_##SUF(const T* f, T* fc, const uint8_t* pid, const T* ktab,           \
+                                                 const T* omd, int ntab, const T* rtab, int nrtab, T w0, int B,  \
+                                                 int H, int W, int ld, long long bs, int ldc, long long bsc,     \
+                                                 T* send, int r0, int r1, int c0, int c1, void* stream) {        \
+    if (!f || !fc || !ktab || !rtab || !omd || !send || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL; \
+    if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;                                                    \
+    if (ntab < 1 || ntab > FEA_MAX_PATTERNS || (ntab > 1 && !pid)) return FEA_EINVAL;                         \
+    if (nrtab != ntab && nrtab != 1) return FEA_EINVAL;                                                      \
+    const bool multi = ntab > 1;                                                                             \
+    if (multi && nrtab == 1) return FEA_EINVAL;                                                              \
+    MgArgs<T> g = mg_args<T>(H, W, ld, bs, B);                                                               \
+    g.f = f; g.out = fc; g.pid = pid; g.ktab = ktab; g.omd = omd; g.ntab = ntab;                              \
+    g.rtab = rtab; g.nrtab = nrtab; g.w = w0; g.Hc = (H + 1) / 2; g.Wc = (W + 1) / 2; g.ldc = ldc;            \
+    g.bsc = bsc;                                                                                             \
+    if (r0 < 0 || r1 <= r0 || c0 < 0 || c1 <= c0 || r1 > g.Hc || c1 > g.Wc) return FEA_EINVAL;               \
+    g.gsend = send; g.gr0 = r0; g.gr1 = r1; g.gc0 = c0; g.gc1 = c1;                                          \
+    g.nstrips = div_up(W - 2, Ovl<T>::S);                                                                    \
+    g.rb = pick_rb(B, g.nstrips, H - 2);                                                                     \
+    g.ntr = div_up(g.Hc - 2, g.rb / 2);                                                                      \
+    const dim3 grid = mg_grid_lin(B, g.ntr, g.nstrips);                                                      \
+    hipStream_t s = (hipStream_t)stream;                                                                     \
+    if (multi) FEA_NT_LAUNCH(k_mg_zero_restrict, T COMMA true)                                               \
+    else FEA_NT_LAUNCH(k_mg_zero_restrict, T COMMA false)                                                    \
+    FEA_LAUNCH_CHECK();                                                                                      \
+  }                                                                                                          \
   extern "C" int fea_mg_sweep_restrict_##SUF(const T* u, const T* f, T* u_out, T* fc, const uint8_t* pid,       \
                                              const T* ktab, const T* omd, int ntab, const T* rtab, int nrtab,    \
                                              T w0, int B, int H, int W, int ld, long long bs, int ldc,          \
@@ -3379,10 +3425,13 @@ static int balanced_units(int B, int nstrips, int rows_u, int k, int ovh, int fa
 #endif
 }
 
+// send: the agglomeration's all-gather send buffer ([B, r1 - r0, c1 - c0]) that also receives f_{l+2}'s block
+// [r0, r1) x [c0, c1) (nullptr: none)
 template <typename T>
 static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const uint8_t* pidc, const T* ktab,
                           const T* omd, int ntab, const T* rtab, int nrtab, T w0, int B, int H, int W, int ld,
-                          long long bs, int ldc, long long bsc, int ldc2, long long bsc2, void* stream) {
+                          long long bs, int ldc, long long bsc, int ldc2, long long bsc2, void* stream,
+                          T* send = nullptr, int r0 = 0, int r1 = 0, int c0 = 0, int c1 = 0) {
   if (!f || !fc || !fc2 || !ktab || !omd || !rtab || B <= 0 || !layout_ok<T>(H, W, ld, bs)) return FEA_EINVAL;
   if (!coarse_ok<T>(H, W, ldc, bsc)) return FEA_EINVAL;
   const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
@@ -3396,6 +3445,10 @@ static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const u
   g.rtab = rtab; g.nrtab = nrtab; g.w = w0;
   g.Hc = Hc; g.Wc = Wc; g.ldc = ldc; g.bsc = bsc;
   g.Hc2 = (Hc + 1) / 2; g.Wc2 = (Wc + 1) / 2; g.ldc2 = ldc2; g.bsc2 = bsc2;
+  if (send) {
+    if (r0 < 0 || r1 <= r0 || c0 < 0 || c1 <= c0 || r1 > g.Hc2 || c1 > g.Wc2) return FEA_EINVAL;
+    g.gsend = send; g.gr0 = r0; g.gr1 = r1; g.gc0 = c0; g.gc1 = c1;
+  }
   g.nstrips = div_up(W - 2, Ovl2<T>::S);
   g.rb = 2 * kRB;
   while (g.rb > kZr2MinRb && (long long)B * g.nstrips * div_up(g.Hc2 - 2, g.rb / 4) < kZr2Waves) g.rb /= 2;
@@ -3415,6 +3468,15 @@ static int zero_restrict2(const T* f, T* fc, T* fc2, const uint8_t* pid, const u
                                              long long bsc, int ldc2, long long bsc2, void* stream) {            \
     return zero_restrict2<T>(f, fc, fc2, pid, pidc, ktab, omd, ntab, rtab, nrtab, w0, B, H, W, ld, bs, ldc, bsc,  \
                              ldc2, bsc2, stream);                                                              \
+  }                                                                                                           \
+  extern "C" int fea_mg_zero_restrict2_send_##SUF(const T* f, T* fc, T* fc2, const uint8_t* pid,                \
+                                                  const uint8_t* pidc, const T* ktab, const T* omd, int ntab,    \
+                                                  const T* rtab, int nrtab, T w0, int B, int H, int W, int ld,   \
+                                                  long long bs, int ldc, long long bsc, int ldc2, long long bsc2, \
+                                                  T* send, int r0, int r1, int c0, int c1, void* stream) {       \
+    if (!send) return FEA_EINVAL;                                                                             \
+    return zero_restrict2<T>(f, fc, fc2, pid, pidc, ktab, omd, ntab, rtab, nrtab, w0, B, H, W, ld, bs, ldc, bsc,  \
+                             ldc2, bsc2, stream, send, r0, r1, c0, c1);                                        \
   }
 FEA_ZR2_API(f32, float)
 FEA_ZR2_API(f64, double)

@@ -67,6 +67,12 @@ struct MidArgs {
   T w;            // down: w0, up: w1
   int k, ntab, nx;
   int TR, TC, ntr, ntc;  // tile size and tiles per dimension (at level a+k down, level a up)
+  // down, gathered top level (a domain-decomposed run's agglomerated coarse problem): f_a is read from the
+  // all-gather's buffer gsrc ([Pr * Pc][B][gcr][gcc]: rank blocks of gcr x gcc interior nodes, rank order) and
+  // each tile places the nodes it owns into the framed f_a (fo[0]) for the later launches — the placement copy
+  // folded into the launch that reads the blocks first
+  const T* gsrc;
+  int gB, gPc, gcr, gcc;
 };
 
 // One region of a level: rows [r0, r0+nr), columns [c0, c0+nc), row-major in LDS.
@@ -201,7 +207,7 @@ __host__ __device__ inline long long mid_up_lds(int k, int TR, int TC, int esz, 
 // ---------------------------------------------------------------------------------------------
 // down: f_a -> f_{a+1} .. f_{a+k}
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool MULTI, int K>
+template <typename T, bool MULTI, int K, bool GATH = false>
 __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
   __shared__ __attribute__((aligned(16))) char smem[kMidLdsBytes];
   FEA_MID_MARK(2 * blockIdx.x);
@@ -292,6 +298,16 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
     const bool cin = lv && c >= 1 && c <= W - 2;
     const T* src = a.f[0] + (long long)b * a.bs[0] + OFF + min(max(c, 0), W - 1);  // top level, row -1
     const int ld0 = a.ld[0];
+    // gathered top level: the lane's column inside its rank block (nodes 1 .. W-1 lie in blocks)
+    const int gcl = min(max(c, 1), W - 1) - 1;
+    const int gbi = GATH ? gcl / a.gcc : 0, gbc = gcl - gbi * a.gcc;
+    auto gload = [&](int y) -> T {
+      const int yy = min(max(y, 1), H - 1) - 1;
+      const int ri = yy / a.gcr, rr = yy - ri * a.gcr;
+      const T v = a.gsrc[(((long long)(ri * a.gPc + gbi) * a.gB + b) * a.gcr + rr) * a.gcc + gbc];
+      return (y >= 1 && y <= H - 1 && c >= 1 && c <= W - 1) ? v : T(0);
+    };
+    T* const place = a.fo[0] + (long long)b * a.bs[0] + OFF + c;
     T* fc = F[j + 1];
     T* go = a.fo[j + 1] + (long long)b * a.bs[j + 1];
     const int ldc = a.ld[j + 1];
@@ -308,7 +324,8 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
 #pragma unroll
       for (int d = 0; d < R; ++d) {
         const int rr = 2 * II0 + d, y = G.r0 + rr;
-        if constexpr (GLOB) fr[d] = src[(long long)(min(max(y, 0), H - 1) + 1) * ld0];
+        if constexpr (GLOB && GATH) fr[d] = gload(y);
+        else if constexpr (GLOB) fr[d] = src[(long long)(min(max(y, 0), H - 1) + 1) * ld0];
         else fr[d] = f[min(rr, G.nr - 1) * G.nc + lane];
         pr[d] = 0;
         if constexpr (MULTI) {
@@ -329,6 +346,16 @@ __global__ __launch_bounds__(kMidThreads) void k_mg_mid_down(MidArgs<T> a) {
         if constexpr (MULTI) {
           pl[d] = shr1z(pr[d]);
           ph[d] = shl1z(pr[d]);
+        }
+      }
+      if constexpr (GLOB && GATH) {
+        {  // placement of the tile's own interior nodes of the gathered top level
+          const bool oc = lv && c >= os_c[0] && c < oe_c[0] && c >= 1 && c <= W - 2;
+#pragma unroll
+          for (int d = 0; d < R; ++d) {
+            const int y = G.r0 + 2 * II0 + d;
+            if (oc && y >= os_r[0] && y < oe_r[0] && y >= 1 && y <= H - 2) place[(long long)(y + 1) * ld0] = fr[d];
+          }
         }
       }
       r[0] = r[R - 1] = T(0);
@@ -745,6 +772,36 @@ static void mid_launch(Kern k1, Kern k2, Kern k3, Kern k4, int k, dim3 grid, voi
                                    k_mg_mid_down<T, true, 3>, k_mg_mid_down<T, true, 4>, k, grid, stream, a);     \
     else mid_launch<T, false>(k_mg_mid_down<T, false, 1>, k_mg_mid_down<T, false, 2>,                             \
                               k_mg_mid_down<T, false, 3>, k_mg_mid_down<T, false, 4>, k, grid, stream, a);        \
+    FEA_LAUNCH_CHECK();                                                                                          \
+  }                                                                                                              \
+  extern "C" int fea_mg_mid_down_gathered_##SUF(const T* const* f, const uint8_t* const* pid, int k, int B, int H, \
+                                                int W, const T* ktab, const T* omd, int ntab, const T* rtab,      \
+                                                int nrtab, T w0, int TR, int TC, const T* gsrc, int Pr, int Pc,    \
+                                                int gcr, int gcc, void* stream) {                                 \
+    MidArgs<T> a = {};                                                                                           \
+    if (!f || !ktab || !omd || !rtab || !gsrc || ntab < 1 || ntab > FEA_MAX_PATTERNS) return FEA_EINVAL;       \
+    if (Pr < 1 || Pc < 1 || gcr < 1 || gcc < 1 || H - 1 != Pr * gcr || W - 1 != Pc * gcc) return FEA_EINVAL;    \
+    const bool multi = ntab > 1;                                                                                 \
+    if ((multi && (!pid || nrtab != ntab)) || (!multi && nrtab != 1)) return FEA_EINVAL;                        \
+    if (mid_fill<T>(a, k, B, H, W, TR, TC)) return FEA_EINVAL;                                                   \
+    if (mid_down_lds(k, TR, TC, (int)sizeof(T), multi) > kMidLdsBytes) return FEA_EINVAL;                       \
+    for (int j = 0; j <= k; ++j) {                                                                               \
+      if (!f[j] || (multi && j < k && !pid[j])) return FEA_EINVAL;                                              \
+      a.f[j] = f[j];                                                                                             \
+      a.fo[j] = const_cast<T*>(f[j]);                                                                            \
+      a.pid[j] = multi && j < k ? pid[j] : nullptr;                                                              \
+    }                                                                                                            \
+    a.ktab = ktab; a.omd = omd; a.xtab = rtab; a.w = w0; a.ntab = ntab; a.nx = nrtab;                           \
+    a.gsrc = gsrc; a.gB = B; a.gPc = Pc; a.gcr = gcr; a.gcc = gcc;                                               \
+    a.ntr = (a.H[k] - 2 + TR - 1) / TR;                                                                          \
+    a.ntc = (a.W[k] - 2 + TC - 1) / TC;                                                                          \
+    const dim3 grid(B * a.ntr * a.ntc);                                                                          \
+    if (multi) mid_launch<T, true>(k_mg_mid_down<T, true, 1, true>, k_mg_mid_down<T, true, 2, true>,           \
+                                   k_mg_mid_down<T, true, 3, true>, k_mg_mid_down<T, true, 4, true>, k, grid,     \
+                                   stream, a);                                                                    \
+    else mid_launch<T, false>(k_mg_mid_down<T, false, 1, true>, k_mg_mid_down<T, false, 2, true>,                 \
+                              k_mg_mid_down<T, false, 3, true>, k_mg_mid_down<T, false, 4, true>, k, grid,        \
+                              stream, a);                                                                         \
     FEA_LAUNCH_CHECK();                                                                                          \
   }                                                                                                              \
   extern "C" int fea_mg_mid_up_##SUF(const T* const* f, const T* e, T* out, const uint8_t* const* pid, int k,   \

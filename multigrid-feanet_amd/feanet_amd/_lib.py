@@ -45,6 +45,8 @@ _SIGS = {
     "mg_sweep": [P, P, P, P, P, P, I, I, I, I, I, LL, P],
     "mg_residual_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_zero_restrict2": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P],
+    "mg_zero_restrict2_send": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P, I, I, I, I, P],
+    "mg_zero_restrict_send": [P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P, I, I, I, I, P],
     "mg_sweep_restrict": [P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P, P, P, P],
     "mg_prolong_sweep": [P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_prolong2": [P, P, P, P, P, P, P, P, P, I, P, I, "S", I, I, I, I, LL, I, LL, I, LL, P],
@@ -59,6 +61,7 @@ _SIGS = {
     "mg_hjac_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, P, I, "S", "S", I, I, I, P],
     # several coarse levels per launch (pointer arrays: ptr_array())
     "mg_mid_down": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
+    "mg_mid_down_gathered": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P, I, I, I, I, P],
     "mg_mid_up": [P, P, P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],
     "mg_hmid_down": [P, P, P, I, I, I, P, P, I, P, I, P, I, "S", I, P],
     "mg_hmid_up": [P, P, P, P, P, I, I, I, P, P, I, P, I, P, I, "S", I, P],

@@ -449,7 +449,7 @@ class DDSolver:
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
                  batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5,
-                 split_join=False):
+                 split_join=False, fold_gather=True):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
         self.graph_min = graph_min
@@ -485,6 +485,10 @@ class DDSolver:
         # captured cycles: the finest join split into border rectangles (run with the halo exchange on a side
         # stream) and the interior (split_join; DDSolver.join_rects)
         self.split_join = split_join
+        # fold_gather (2-D blocks, communicators with a device pack): the agglomeration's staging and placement copies
+        # run inside the restriction that computes f_Ld and the coarse plan's first launch (DDSolver._send_form /
+        # _gathered_form) instead of as copy launches of their own
+        self.fold_gather = fold_gather
         self._segs = {}
         self._graphs = {}
         self._state = "a"
@@ -589,11 +593,18 @@ class DDSolver:
                 continue
             if st[0] == "gather" and self.P > 1:
                 if fold and self.Pc > 1 and segs and segs[-1][0] == "k":
-                    # 2-D blocks: the owned block's staging copy ends the kernel segment before the
-                    # all-gather and the placement starts the one after it (captured, not eager launches)
+                    # 2-D blocks: the owned block goes to the all-gather's send buffer and the gathered blocks into
+                    # the coarse f.  Both fold into the launches around the all-gather where those are the zero-
+                    # guess restriction that computes f_Ld (its _send form stores the block too) and the coarse
+                    # plan's mid_down (its _gathered form reads the blocks and places them); otherwise a staging
+                    # copy ends the kernel segment before the all-gather and a placement copy starts the one after.
                     tgt = self.gather_target()
-                    segs[-1][1].append(("copy", (self._gsend, self.gather_source())))
-                    place = ("copy", self.gather_place_views(tgt))
+                    sent = self._send_form(segs[-1][1][-1]) if self.fold_gather else None
+                    if sent is not None:
+                        segs[-1][1][-1] = sent
+                    else:
+                        segs[-1][1].append(("copy", (self._gsend, self.gather_source())))
+                    place = ("place", self.gather_place_views(tgt))
                     segs.append(("c", ("gather", True), False))
                 else:
                     segs.append(("c", st, False))
@@ -612,7 +623,12 @@ class DDSolver:
                 if direct is not None:
                     launches, direct = [self._read_coarse_in_place(launches[0])], None
             if place is not None:
-                launches, place = [place] + launches, None
+                gath = self._gathered_form(launches[0]) if self.fold_gather else None
+                if gath is not None:
+                    launches = [gath] + launches[1:]
+                else:
+                    launches = [("copy", place[1])] + launches
+                place = None
             if segs and segs[-1][0] == "k":
                 segs[-1][1].extend(launches)
                 if lvl0:
@@ -628,6 +644,31 @@ class DDSolver:
                         segs[i - 1][1].append(("fn", f))
                     segs[i] = ("c", ("exchanges", st[1], True), False)
         return [(kind, _as_rect_copies(st), lvl0) if kind == "k" else (kind, st, lvl0) for kind, st, lvl0 in segs]
+
+    def _send_form(self, launch):
+        """The _send form of the zero-guess restriction `launch` when it computes f_Ld (2-D blocks: it then also
+        stores this rank's block of f_Ld into the all-gather's send buffer, fea_mg_zero_restrict2_send /
+        fea_mg_zero_restrict_send), else None."""
+        name, args = launch
+        f_ld = self.local.levels[self.Ld].f.data_ptr()
+        pl, ql = self.parts[self.Ld], self.cparts[self.Ld]
+        blk = (self._gsend.data_ptr(), pl.lo, pl.lo + self.part.rows_per_rank(self.Ld), ql.lo,
+               ql.lo + self.part.cols_per_rank(self.Ld))
+        if name == "mg_zero_restrict2" and args[2] == f_ld:
+            return ("mg_zero_restrict2_send", tuple(args) + blk)
+        if name == "mg_residual_restrict" and args[3] == f_ld and args[0] is None and args[2] is None:
+            # (u, f, v_out, fc, pid, ktab, omd, ntab, rtab, nrtab, w0, geometry ...) -> (f, fc, pid, ..., geometry ...)
+            return ("mg_zero_restrict_send", (args[1], args[3]) + tuple(args[4:]) + blk)
+        return None
+
+    def _gathered_form(self, launch):
+        """The coarse plan's first launch in its _gathered form when it is the mid_down over the coarse top level (it
+        then reads f_Ld's blocks from the all-gather's buffer and places them, fea_mg_mid_down_gathered), else None."""
+        name, args = launch
+        if name != "mg_mid_down" or args[0].arr[0] != self.coarse.levels[0].f.data_ptr():
+            return None
+        c, cc = self.part.rows_per_rank(self.Ld), self.part.cols_per_rank(self.Ld)
+        return ("mg_mid_down_gathered", tuple(args) + (self._gstage.data_ptr(), self.Pr, self.Pc, c, cc))
 
     def _scatter_direct(self, st, nxt):
         """Can the scatter step `st` (coarse solution -> level Ld's buffer st[1]) be dropped, the next step reading

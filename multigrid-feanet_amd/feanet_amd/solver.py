@@ -127,8 +127,12 @@ class MultigridSolver:
 
     MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
     #                       streaming kernels win: tools/lab/mid_lab.py)
+    MID_NODES_MULTI = 20000  # two-material problems: <= 129^2, i.e. no group of two levels above the 65^2 tail — their
+    #                          LDS-tile launches pay per-node table lookups, the streaming two-level kernels run instead
+    #                          (C3 2049^2 cycle 92.0 -> 89.3 us against 513^2, 92.7 with 257^2: profiles/r06_ab/c3_mid.txt)
     MID_MIN_TILES = 200   # workgroups a multi-level launch should give the 256 CUs
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
+    HMID_NODES = 300000   # learned-smoother levels paired into the HJac two-level launches: <= 513^2 nodes
     HMID_MIN_TILES = 64   # workgroups an HJac two-level launch should give the CUs (one per CU: LDS)
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
@@ -463,9 +467,9 @@ class MultigridSolver:
 
     def _pick_hmid(self):
         """(a, T_down, T_up) for the HJac levels paired into two-level launches: streamed coarse levels (a >= 1,
-        above the HJac tail) of <= MID_NODES nodes, paired from the coarse end upward."""
+        above the HJac tail) of <= HMID_NODES nodes, paired from the coarse end upward."""
         top = self.hjac_tail_from if self.hjac_tail_from is not None else self.L - 1
-        el = [l for l in range(1, top) if self.B * self.levels[l].H * self.levels[l].W <= self.MID_NODES]
+        el = [l for l in range(1, top) if self.B * self.levels[l].H * self.levels[l].W <= self.HMID_NODES]
         pairs = []
         hi = len(el)
         while hi >= 2:
@@ -481,7 +485,7 @@ class MultigridSolver:
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
-        cap = self.MID_NODES
+        cap = self.MID_NODES_MULTI if self.ntab > 1 else self.MID_NODES
         el = sorted(l for l in levels
                     if self.B * self.levels[l].H * self.levels[l].W <= cap and l + 1 < self.L)
         groups = []

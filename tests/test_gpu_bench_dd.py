@@ -74,3 +74,5 @@ def test_bench_gpus_flag_launches_ranks():
     dm = rec["config"]["dd_mode"]
     assert dm["backend"] == "gloo" and dm["cycle_graphs"].startswith("segments")  # gloo is never captured
     assert not any(m["capture_requested"] for m in rec["dd_modes"])
+    timed = [m for m in rec["dd_modes"] if m["status"] == "ok"]
+    assert len(timed) >= 3 and all(m["dd_parity"]["bitwise_equal"] for m in timed), rec["dd_modes"]

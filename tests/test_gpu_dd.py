@@ -375,3 +375,83 @@ def test_dd_capture_refusal_is_collective(refuse):
         L0 = s.local.levels[0]
         outs.append(L0.view(L0.buf(s._state)).clone())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("kind,problem", [("zr2", "poisson"), ("zr1", "poisson"), ("zr2", "interface"),
+                                          ("zr1", "interface")])
+def test_restriction_send_forms_bitwise(kind, problem):
+    """fea_mg_zero_restrict2_send / fea_mg_zero_restrict_send (the agglomeration's send buffer filled by the
+    restriction that computes f_Ld, DDSolver._send_form): the level outputs bitwise the plain launches', and the
+    send buffer holds exactly the requested block of the output level (zeros where the block leaves its interior)."""
+    from feanet_amd import _lib
+    from feanet_amd.solver import MultigridSolver
+    T = torch.float64
+    s = MultigridSolver(512, problem=problem, dtype=T)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    s.set_rhs(f=torch.randn(1, 1, 513, 513, device="cuda", dtype=T, generator=g))
+    stream = torch.cuda.current_stream().cuda_stream
+    if kind == "zr2":
+        name, args = s.bind_step(("resid_restrict2", 0))
+        out = s.levels[2]
+    else:
+        name, args = s.bind_step(("resid_restrict", 0, None, None))
+        out = s.levels[1]
+    r0, r1, c0, c1 = 5, out.H, 3, 40  # a block touching the last (boundary) row
+    _lib.call(name, T, *args, stream)
+    ref = out.view(out.f).clone()
+    ref1 = s.levels[1].view(s.levels[1].f).clone()
+    for Lv in s.levels[1:3]:
+        Lv.f.zero_()
+    send = torch.zeros((1, r1 - r0, c1 - c0), dtype=T, device="cuda")
+    if kind == "zr2":
+        _lib.call("mg_zero_restrict2_send", T, *args, send.data_ptr(), r0, r1, c0, c1, stream)
+    else:
+        _lib.call("mg_zero_restrict_send", T, args[1], args[3], *args[4:], send.data_ptr(), r0, r1, c0, c1, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(out.f), ref) and torch.equal(s.levels[1].view(s.levels[1].f), ref1)
+    exp = ref[:, r0:r1, c0:c1].clone()
+    exp[:, out.H - 1 - r0:, :] = 0  # the output level's boundary row is not written
+    assert torch.equal(send, exp)
+
+
+@pytest.mark.parametrize("grid,B", [((2, 2), 1), ((4, 2), 1), ((2, 4), 2)])
+def test_mid_down_gathered_bitwise(grid, B):
+    """fea_mg_mid_down_gathered (DDSolver._gathered_form): level a's f read from the all-gather's rank blocks
+    ([Pr * Pc][B][c_r][c_c]) and placed into the framed f_a by the owning tiles — outputs bitwise fea_mg_mid_down on
+    the placed field, and the placed interior equal to it."""
+    from feanet_amd import _lib
+    from feanet_amd.solver import MultigridSolver
+    T = torch.float64
+    n = 256
+    Pr, Pc = grid
+    cr, cc = n // Pr, n // Pc
+    s = MultigridSolver(n, dtype=T, batch=B, zero_start=True)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    f = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=T, generator=g)
+    f[:, :, 0] = 0
+    f[:, :, -1] = 0
+    f[:, :, :, 0] = 0
+    f[:, :, :, -1] = 0
+    s.set_rhs(f=f)
+    plan, _ = s._plan("a")
+    name, args = plan[0]
+    assert name == "mg_mid_down", [p[0] for p in plan]
+    k = args[2]
+    stream = torch.cuda.current_stream().cuda_stream
+    _lib.call(name, T, *args, stream)
+    refs = [s.levels[j].view(s.levels[j].f).clone() for j in range(k + 1)]
+    # the gathered blocks: rank r = ri * Pc + ci holds nodes 1 + ri cr .., 1 + ci cc ..
+    L0 = s.levels[0]
+    v = L0.view(L0.f)
+    blocks = torch.stack([v[:, 1 + ri * cr:1 + (ri + 1) * cr, 1 + ci * cc:1 + (ci + 1) * cc]
+                          for ri in range(Pr) for ci in range(Pc)]).contiguous()
+    for j in range(k + 1):
+        s.levels[j].f.zero_()
+    _lib.call("mg_mid_down_gathered", T, *args, blocks.data_ptr(), Pr, Pc, cr, cc, stream)
+    torch.cuda.synchronize()
+    got0 = s.levels[0].view(s.levels[0].f)
+    assert torch.equal(got0[:, 1:-1, 1:-1], refs[0][:, 1:-1, 1:-1])
+    for j in range(1, k + 1):
+        assert torch.equal(s.levels[j].view(s.levels[j].f), refs[j]), j

@@ -140,6 +140,8 @@ def main():
                     help="one graph per kernel segment between communication steps (the path of communicators that "
                          "cannot be captured) instead of whole captured cycles")
     ap.add_argument("--graph-min", type=int, default=None, help="DDSolver(graph_min=): shorter segments eager")
+    ap.add_argument("--no-fold-gather", action="store_true",
+                    help="DDSolver(fold_gather=False): the agglomeration's staging / placement as copy launches")
     ap.add_argument("--split", action="store_true",
                     help="captured cycles with the border / interior split of the finest join (DDSolver split_join)")
     args = ap.parse_args()
@@ -167,7 +169,7 @@ def main():
                 comm = NullComm() if args.no_pack else PackComm()
                 comm.capturable = not args.segments
                 s = DDSolver(n, n, r, P, comm=comm, agglomerate=Ld, grid=(Pr, Pc),
-                             graph=not args.no_graph, split_join=args.split,
+                             graph=not args.no_graph, split_join=args.split, fold_gather=not args.no_fold_gather,
                              **({} if args.graph_min is None else {"graph_min": args.graph_min}))
             except ValueError as e:
                 print(f"P={P} {Pr}x{Pc} Ld={Ld}: not partitionable ({e})", flush=True)
