@@ -125,11 +125,13 @@ class MultigridSolver:
             to single-level launches run as one each (fea_mg_zero_restrict2 / fea_mg_prolong2, bitwise the two).
     """
 
-    MID_NODES = 300000    # latency-bound levels: <= 513^2 nodes per launch (at 1025^2 the per-level
-    #                       streaming kernels win: tools/lab/mid_lab.py)
-    MID_NODES_MULTI = 20000  # two-material problems: <= 129^2, i.e. no group of two levels above the 65^2 tail — their
-    #                          LDS-tile launches pay per-node table lookups, the streaming two-level kernels run instead
-    #                          (C3 2049^2 cycle 92.0 -> 89.3 us against 513^2, 92.7 with 257^2: profiles/r06_ab/c3_mid.txt)
+    MID_NODES = 20000     # levels with <= this many nodes (B*H*W) may go to the LDS-tile multi-level launches (groups
+    #                       of >= 2 consecutive levels above the coarse tail).  Round 6: 20000 (<= 129^2, which forms no
+    #                       group above the 65^2 tail, so the standard plans run the streaming two-level kernels on
+    #                       every level above it) — metric V-cycle 132.6 -> 128.8 us, C2 35.9 -> 33.6, C4 grid 528 ->
+    #                       519, C3 92.0 -> 90.0, C5 level, DD 8-rank projection 108.9 -> 104.6 against 300000 (<= 513^2,
+    #                       rounds 2-5), once this round's task heights had sped the two-level kernels up
+    #                       (profiles/r06_ab/mid_nodes.txt).  Larger values still select the multi-level launches (bitwise).
     MID_MIN_TILES = 200   # workgroups a multi-level launch should give the 256 CUs
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
     HMID_NODES = 300000   # learned-smoother levels paired into the HJac two-level launches: <= 513^2 nodes
@@ -485,7 +487,7 @@ class MultigridSolver:
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
-        cap = self.MID_NODES_MULTI if self.ntab > 1 else self.MID_NODES
+        cap = self.MID_NODES
         el = sorted(l for l in levels
                     if self.B * self.levels[l].H * self.levels[l].W <= cap and l + 1 < self.L)
         groups = []

@@ -416,7 +416,7 @@ def test_restriction_send_forms_bitwise(kind, problem):
 
 
 @pytest.mark.parametrize("grid,B", [((2, 2), 1), ((4, 2), 1), ((2, 4), 2)])
-def test_mid_down_gathered_bitwise(grid, B):
+def test_mid_down_gathered_bitwise(grid, B, monkeypatch):
     """fea_mg_mid_down_gathered (DDSolver._gathered_form): level a's f read from the all-gather's rank blocks
     ([Pr * Pc][B][c_r][c_c]) and placed into the framed f_a by the owning tiles — outputs bitwise fea_mg_mid_down on
     the placed field, and the placed interior equal to it."""
@@ -426,6 +426,7 @@ def test_mid_down_gathered_bitwise(grid, B):
     n = 256
     Pr, Pc = grid
     cr, cc = n // Pr, n // Pc
+    monkeypatch.setattr(MultigridSolver, "MID_NODES", 300000)  # a coarse plan that starts with mid_down
     s = MultigridSolver(n, dtype=T, batch=B, zero_start=True)
     g = torch.Generator(device="cuda")
     g.manual_seed(5)

@@ -484,3 +484,37 @@ def test_hmid_kernels_vs_per_level_calls(T, problem, m, n, B, nl):
         got = get(lv[0], "b")
         assert torch.equal(got, ref_up), (tu, (got - ref_up).abs().max().item())
         assert (got[:, 0] == 7).all() and (got[:, -1] == 7).all() and (got[:, :, 0] == 7).all()
+
+
+def test_hjac_c3_interface_vs_oracle():
+    """The learned smoother on BASELINE C3's two-material problem (SURVEY §8f row 1 on MM_Interface): 2049^2 fp64
+    circle inclusion (contrast 20), the learned ratio R / P / w of FEANet/multigrid.py, F = ones, every sweep an
+    HRelax with the shipped HNet weights — against the oracle's MultiGrid.Step with HRelax sweeps
+    (M-FEANet-mg_test.ipynb:147-155, :27346-27372) on the oracle's own pattern maps (tests/golden/c3_pattern_maps.npz):
+    three cycles from zero, 1e-10 of max|u| after each."""
+    import os
+    from feanet_amd.solver import MultigridSolver
+    here = os.path.dirname(__file__)
+    n = 2048
+    w = np.load(os.path.join(here, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
+    hw = np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+    rp = np.load(os.path.join(here, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
+    s = MultigridSolver(n, problem="interface", dtype=torch.float64, smoother="hjac", hnet=hw, R=rp["R"][0],
+                        P=rp["P"][:, 0], w=rp["w"])
+    s.set_rhs(F=torch.ones(1, 1, n + 1, n + 1, device="cuda", dtype=torch.float64))
+    s.load()
+    maps = np.load(os.path.join(here, "golden", "c3_pattern_maps.npz"))
+    pids = {int(k[4:]): maps[k] for k in maps.files if k.startswith("pid_")}
+    mg = orc.OracleMultigrid(n, "interface", np.float64, levels=s.L, pids=pids,
+                             rtab=np.broadcast_to(np.asarray(rp["R"][0], np.float32), (16, 3, 3)),
+                             ptab=np.asarray(rp["P"][:, 0], np.float32), w=tuple(float(x) for x in rp["w"]))
+    for l in mg.levels:
+        l.sweep = (lambda ll, o: (lambda v, ff: (lambda j: j + orc.hnet(j - v, ll.geo, hw))(o(v, ff))))(l, l.sweep)
+    f = orc.conv3x3(np.ones((1, n + 1, n + 1)), orc.fnet_stencil(2.0 / n))
+    v = np.zeros((1, n + 1, n + 1))
+    for k in range(3):
+        s.vcycle()
+        v = mg.step(v, f)
+        got = s.solution().cpu().numpy()[:, 0]
+        err = np.abs(got - v).max() / max(1.0, np.abs(v).max())
+        assert err < 1e-10, (k, err)

@@ -118,18 +118,14 @@ def test_mid_rejects_oversized_tiles():
                   rt.data_ptr(), 1, 1.0, 200, 200, None)
 
 
-@pytest.mark.parametrize("problem,n,B,T,cap", [("poisson", 1024, 1, torch.float64, None),
-                                                ("poisson", 2048, 1, torch.float64, None),
-                                                ("poisson", 1024, 2, torch.float32, None),
-                                                ("interface", 1024, 1, torch.float64, 300000)])
-def test_solver_mid_bitwise(problem, n, B, T, cap, monkeypatch):
-    """MultigridSolver with the multi-level launches == without (bitwise), single and joined cycles.  cap: the
-    two-material problem's grouping threshold (MID_NODES_MULTI; its default, 129^2, forms no group of two levels
-    above the 65^2 tail, so the two-material plans run no multi-level launch — 300000 exercises them on levels up to
-    513^2)."""
+@pytest.mark.parametrize("problem,n,B,T", [("poisson", 1024, 1, torch.float64), ("poisson", 2048, 1, torch.float64),
+                                            ("poisson", 1024, 2, torch.float32), ("interface", 1024, 1, torch.float64)])
+def test_solver_mid_bitwise(problem, n, B, T, monkeypatch):
+    """MultigridSolver with the multi-level launches == without (bitwise), single and joined cycles.  The default
+    grouping threshold (MID_NODES, <= 129^2) forms no group above the 65^2 tail; 300000 (the rounds-2-5 default,
+    <= 513^2) makes the solver use them."""
     from feanet_amd.solver import MultigridSolver
-    if cap is not None:
-        monkeypatch.setattr(MultigridSolver, "MID_NODES_MULTI", cap)
+    monkeypatch.setattr(MultigridSolver, "MID_NODES", 300000)
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
     f = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=T, generator=g)
