@@ -432,6 +432,17 @@ int fea_mg_coarse_tail_f64(const double* f_t, double* v_t, int Ht, int Wt, int n
                            const uint8_t* pid_levels, const double* ktab, const double* omd, int ntab,
                            const double* rtab, const double* ptab, double w0, double w1, int nu1, int nu2,
                            int q2, int B, void* stream);
+/* The coarse tail with the level above it (level X: Hx = 2 Ht - 1 rows, Wx = 2 Wt - 1 <= 129 columns, framed f_x /
+ * v_x with ld_x, bs_x) in the same launch: X's zero-guess restriction (fea_mg_residual_restrict with u = NULL and no
+ * iterate stored) into the tail's LDS, the tail's nlev levels, then X's recomputed-iterate prolongation + sweep
+ * (fea_mg_prolong_sweep with u = NULL) into v_x's interior — bitwise those three launches
+ * (FEANet/multigrid.py:165-183 for the levels below the one above X).  Single pattern (ntab == 1), V(1,1). */
+int fea_mg_coarse_tail_ext_f32(const float* f_x, float* v_x, int Hx, int Wx, int ld_x, long long bs_x, int nlev,
+                               const float* ktab, const float* omd, int ntab, const float* rtab, const float* ptab,
+                               float w0, float w1, int B, void* stream);
+int fea_mg_coarse_tail_ext_f64(const double* f_x, double* v_x, int Hx, int Wx, int ld_x, long long bs_x, int nlev,
+                               const double* ktab, const double* omd, int ntab, const double* rtab,
+                               const double* ptab, double w0, double w1, int B, void* stream);
 /* LDS bytes the coarse tail needs for (Ht, Wt, nlev); 0 if unsupported.  Must be <= 159 KiB. */
 size_t fea_mg_coarse_tail_lds_bytes(int Ht, int Wt, int nlev, int elem_size, int multi);
 

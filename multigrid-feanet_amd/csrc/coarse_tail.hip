@@ -13,6 +13,8 @@
 // nu1 + nu2 sweeps; q2 = MM_Interface_error.ipynb's grids[0] pre-smoothing, i.e. none here).
 #include "fea_common.h"
 
+#include <utility>
+
 namespace fea {
 
 constexpr int kTailThreads = 1024;
@@ -97,7 +99,7 @@ constexpr bool kTailLateSync = FEA_TAIL_LATE_SYNC != 0;
 
 // HT != 0: the grid is HT x HT with NLEV levels, known at compile time (every BASELINE configuration
 // ends in the 65^2 .. 3^2 tail), so level sizes, offsets and rows per wave fold into immediates.
-template <typename T, bool MULTI, int HT = 0>
+template <typename T, bool MULTI, int HT = 0, bool EXT = false>
 struct TailFast {
   const TailArgs<T>& a;
   T* es;               // per-level corrections (up-sweep outputs), level regions like fs
@@ -280,7 +282,7 @@ struct TailFast {
       const T kv = Kx(j, vl, v, vr, ql, q, qr);
       const T w = keep(omega(q[j]) * (fr[j] - kv) + v[j]);
       if (inside(H, N, y)) {
-        if (k == 0) vg[(long long)y * ld + lane] = w;
+        if (k == 0 && !EXT) vg[(long long)y * ld + lane] = w;
         else es[o + y * N + lane] = w;
       }
     }
@@ -350,7 +352,7 @@ struct TailFast {
       const T kx = Kx(j, xl, x, xr, ql, q, qr);
       const T w = keep(omega(q[j]) * (fr[j] - kx) + x[j]);
       if (inside(H, N, y)) {
-        if (k == 0) vg[(long long)y * ld + lane] = w;
+        if (k == 0 && !EXT) vg[(long long)y * ld + lane] = w;
         else es[o + y * N + lane] = w;
       }
     }
@@ -390,7 +392,7 @@ struct TailFast {
   }
 };
 
-template <typename T, bool MULTI, int HT = 0, int NLEV = 0>
+template <typename T, bool MULTI, int HT = 0, int NLEV = 0, bool EXT = false>
 __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, const T* ktb, const T* rtb,
                                           const T* ptb, const uint8_t* pl, int wv, int lane
 #ifdef FEA_TAIL_TRACE
@@ -399,7 +401,7 @@ __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, co
 ) {
   const int nlev = NLEV ? NLEV : a.nlev;
   const long long s0 = (long long)blockIdx.x * a.bs_t + (128 / (int)sizeof(T) - 1) + a.ld_t;
-  TailFast<T, MULTI, HT> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
+  TailFast<T, MULTI, HT, EXT> t{a, es, fs, ktb, rtb, ptb, pl, a.f_t + s0, a.v_t + s0, a.ld_t, wv, lane};
   if constexpr (!MULTI) {  // single-pattern tables in registers (uniform loads)
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
@@ -413,7 +415,7 @@ __device__ __forceinline__ void tail_fast(const TailArgs<T>& a, T* es, T* fs, co
   // (NLEV != 0: the level loops unroll, so k, the level sizes and offsets are constants in every phase)
   int o = 0;
   auto down = [&](int k) {
-    if (k == 0) t.template down<true>(k, o);
+    if (k == 0 && !EXT) t.template down<true>(k, o);  // (EXT: level 0's f is already in LDS)
     else t.template down<false>(k, o);
     o += t.Hk(k) * t.Nk(k);
     FEA_TAIL_SYNC();
@@ -645,6 +647,249 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The tail extended by ONE streamed level on top (fea_mg_coarse_tail_ext).  Level X (2 Ht - 1 rows x
+// 2 Wt - 1 columns, framed in HBM) goes down and up inside the tail's launch: its zero-guess restriction
+// (k_mg_zero_restrict: v = omd f, f_t = w0 R(f - K v)) writes level t's right-hand side straight into the
+// tail's LDS before the sub-cycle, and its recomputed-iterate prolongation + sweep (k_mg_prolong_zu_ovl:
+// x = omd f + w1 P e_t, v_X = omd (f - K x) + x) reads level t's correction from LDS after it — two launches
+// of the 129^2 level (~5 us each, a boundary plus a row chain on a few waves) and the HBM round trips of f_t
+// and v_t disappear.  Every node value is the same expression, in the same order, as in those streaming kernels
+// (bitwise: tests/test_gpu_mg.py::test_coarse_tail_ext_bitwise).  Lane L holds level X's columns 2L+1, 2L+2 (one
+// aligned 16-B fp64 / 8-B fp32 vector per row; its outer neighbours by DPP); the 16 waves split the rows.
+// Single pattern, V(1,1) (the streaming kernels' zero-guess forms).
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+struct ExtArgs {
+  const T* f;  // level X right-hand side (framed)
+  T* v;        // level X iterate out (framed; interior written)
+  int H, W, ld;
+  long long bs;
+};
+
+template <typename T>
+struct ExtV {  // a row at the lane's columns and their neighbours: a[0..3] = columns 2L .. 2L+3
+  T a[4];
+};
+template <typename T>
+__device__ __forceinline__ ExtV<T> ext_win(T x0, T x1) {  // (own_row of framed_ops.hip)
+  ExtV<T> w;
+  w.a[1] = x0;
+  w.a[2] = x1;
+  w.a[0] = shr1z(x1);
+  w.a[3] = shl1z(x0);
+  return w;
+}
+// (K x) at the lane's column k (0: 2L+1, 1: 2L+2): kapply's taps and order (framed_ops.hip)
+template <typename T>
+__device__ __forceinline__ T ext_k(const ExtV<T>& w0, const ExtV<T>& w1, const ExtV<T>& w2, int k,
+                                   const T (&ks)[9]) {
+  T acc = ks[0] * w0.a[k];
+  acc += ks[1] * w0.a[k + 1];
+  acc += ks[2] * w0.a[k + 2];
+  acc += ks[3] * w1.a[k];
+  acc += ks[4] * w1.a[k + 1];
+  acc += ks[5] * w1.a[k + 2];
+  acc += ks[6] * w2.a[k];
+  acc += ks[7] * w2.a[k + 1];
+  acc += ks[8] * w2.a[k + 2];
+  return acc;
+}
+// crow_term (framed_ops.hip) at the lane's column k from a coarse row's values at columns L (ea) and L+1 (eb)
+template <typename T>
+__device__ __forceinline__ T ext_ct(T ea, T eb, int ky, int k, const T (&ps)[9]) {
+  if (k == 1) return ps[ky * 3 + 1] * eb;  // even fine column 2L+2: coarse node L+1, kx = 1
+  T t = ps[ky * 3 + 2] * ea;              // odd fine column 2L+1: coarse nodes L (kx = 2) and L+1 (kx = 0)
+  t += ps[ky * 3 + 0] * eb;
+  return t;
+}
+template <typename Fn, int... J>
+__device__ __forceinline__ void ext_unroll(Fn&& fn, std::integer_sequence<int, J...>) {  // fn(1) .. fn(PER)
+  (fn(std::integral_constant<int, J + 1>{}), ...);
+}
+template <typename T>
+__device__ __forceinline__ void ext_load(const T* p, T& x0, T& x1) {
+  typedef T v2 __attribute__((ext_vector_type(2)));
+  const v2 v = *reinterpret_cast<const v2*>(p);
+  x0 = v[0];
+  x1 = v[1];
+}
+
+// level X -> fs0 (level t's right-hand side, Ht x Wt, pitch Wt, interior written): coarse rows [I0, I1) per wave.
+// The rows stream through a 3-row window (all loads issued first); every second residual row closes a coarse row.
+template <typename T>
+__device__ __forceinline__ void ext_down(const TailArgs<T>& a, const ExtArgs<T>& x, T* fs0, int Ht, int Wt, int wv,
+                                         int lane) {
+  constexpr int PER = 4, R = 2 * PER + 3;  // Ht - 2 <= 63 coarse rows over 16 waves
+  constexpr int NW = kTailThreads / 64;
+  const int per = (Ht - 2 + NW - 1) / NW;
+  const int I0 = 1 + wv * per, I1 = min(Ht - 1, I0 + per);
+  if (I0 >= I1) return;  // wave-uniform
+  const int H = x.H, W = x.W;
+  const int yb = 2 * I0 - 2;  // fine rows yb .. yb + R - 1
+  const int c0 = 2 * lane + 1;
+  // lanes past the grid load the last interior pair (masked; their values only feed masked neighbours)
+  const T* fb = x.f + (long long)blockIdx.x * x.bs + (128 / (int)sizeof(T) - 1) + min(c0, W - 2);
+  T f0[R], f1[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) ext_load(fb + (long long)(min(yb + j, H - 1) + 1) * x.ld, f0[j], f1[j]);
+  T ks[9], rs[9];
+#pragma unroll
+  for (int d = 0; d < 9; ++d) {
+    ks[d] = a.ktab[d];
+    rs[d] = a.rtab[d];
+  }
+  const T om = a.omd[0], w0 = a.w0;
+  const bool cin0 = c0 <= W - 2, cin1 = c0 + 1 <= W - 2;
+  auto vrow = [&](int j) {
+    const int y = yb + j;
+    const bool rin = y >= 1 && y <= H - 2;
+    return ext_win<T>((rin && cin0) ? om * f0[j] : T(0), (rin && cin1) ? om * f1[j] : T(0));
+  };
+  ExtV<T> va = vrow(0), vb = vrow(1);
+  T ra[3], rb[3];  // the last two residual rows at columns 2L+1, 2L+2, 2L+3 (odd row 2I-1, then even row 2I)
+  const int J = lane + 1;  // coarse column of fine column 2L+2
+#pragma unroll
+  for (int j = 1; j < R - 1; ++j) {
+    const ExtV<T> vc = vrow(j + 1);
+    T r[3];
+    r[0] = f0[j] - ext_k<T>(va, vb, vc, 0, ks);
+    r[1] = f1[j] - ext_k<T>(va, vb, vc, 1, ks);
+    r[2] = shl1z(r[0]);
+    va = vb;
+    vb = vc;
+    if (j >= 3 && (j & 1)) {  // rows j-2, j-1, j = 2I-1, 2I, 2I+1 with I = I0 + (j-3)/2
+      const int I = I0 + (j - 3) / 2;
+      if (I >= I1) break;  // wave-uniform
+      T acc = rs[0] * ra[0];
+      acc += rs[1] * ra[1];
+      acc += rs[2] * ra[2];
+      acc += rs[3] * rb[0];
+      acc += rs[4] * rb[1];
+      acc += rs[5] * rb[2];
+      acc += rs[6] * r[0];
+      acc += rs[7] * r[1];
+      acc += rs[8] * r[2];
+      if (J <= Wt - 2) fs0[I * Wt + J] = w0 * acc;
+    }
+    if (j & 1) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ra[k] = r[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) rb[k] = r[k];
+    }
+  }
+}
+
+// es0 (level t's correction, Ht x Wt, pitch Wt, interior valid) -> level X's iterate on fine rows [y0, y1) per wave
+template <typename T>
+__device__ __forceinline__ void ext_up(const TailArgs<T>& a, const ExtArgs<T>& x, const T* es0, int Ht, int Wt, int wv,
+                                       int lane) {
+  constexpr int PER = 8, R = PER + 2;  // x rows y0-1 .. y0+PER
+  constexpr int NW = kTailThreads / 64;
+  const int H = x.H, W = x.W;
+  const int per = 2 * ((H - 2 + 2 * NW - 1) / (2 * NW));  // even: y0 - 1 is even on every wave
+  const int y0 = 1 + wv * per, y1 = min(H - 1, y0 + per);
+  if (y0 >= y1) return;  // wave-uniform
+  const int c0 = 2 * lane + 1;
+  const long long boff = (long long)blockIdx.x * x.bs + (128 / (int)sizeof(T) - 1);
+  const T* fb = x.f + boff + min(c0, W - 2);
+  T f0[R], f1[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) ext_load(fb + (long long)(min(y0 - 1 + j, H - 1) + 1) * x.ld, f0[j], f1[j]);
+  const int cb = (y0 - 1) >> 1;
+  // coarse row cb + m at columns L (ea) and L+1 (eb), read from LDS where used (0 off the interior, as the
+  // framed zeros)
+  const bool ja = lane >= 1 && lane <= Wt - 2, jb = lane + 1 <= Wt - 2;
+  const int la = min(lane, Wt - 1), lb = min(lane + 1, Wt - 1);
+  auto ea = [&](int m) {
+    const int I = cb + m;
+    const T v = es0[min(I, Ht - 1) * Wt + la];
+    return (I >= 1 && I <= Ht - 2 && ja) ? v : T(0);
+  };
+  auto eb = [&](int m) {
+    const int I = cb + m;
+    const T v = es0[min(I, Ht - 1) * Wt + lb];
+    return (I >= 1 && I <= Ht - 2 && jb) ? v : T(0);
+  };
+  T ks[9], ps[9];
+#pragma unroll
+  for (int d = 0; d < 9; ++d) {
+    ks[d] = a.ktab[d];
+    ps[d] = a.ptab[d];
+  }
+  const T om = a.omd[0], w1 = a.w1;
+  const bool cin0 = c0 <= W - 2, cin1 = c0 + 1 <= W - 2;
+  auto xrow = [&](auto jc) {  // x of row y0 - 1 + j (its parity is j's)
+    constexpr int j = decltype(jc)::value;
+    const int y = y0 - 1 + j;
+    const bool rin = y >= 1 && y <= H - 2;
+    T xv[2];
+    xv[0] = (rin && cin0) ? om * f0[j] : T(0);
+    xv[1] = (rin && cin1) ? om * f1[j] : T(0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if constexpr ((j & 1) == 0) {
+        xv[k] += w1 * ext_ct<T>(ea(j / 2), eb(j / 2), 1, k, ps);
+      } else {
+        const T t = ext_ct<T>(ea(j / 2), eb(j / 2), 2, k, ps) + ext_ct<T>(ea(j / 2 + 1), eb(j / 2 + 1), 0, k, ps);
+        xv[k] += w1 * t;
+      }
+    }
+    return ext_win<T>(xv[0], xv[1]);
+  };
+  T* vb_ = x.v + boff + c0;
+  ExtV<T> A = xrow(std::integral_constant<int, 0>{}), B = xrow(std::integral_constant<int, 1>{});
+  auto emit = [&](auto jc) {  // row y0 - 1 + j from the windows j-1 (A), j (B), j+1 (C)
+    constexpr int j = decltype(jc)::value;
+    const ExtV<T> Cw = xrow(std::integral_constant<int, j + 1>{});
+    const int y = y0 - 1 + j;
+    if (y < y1) {  // wave-uniform
+      T o[2];
+      o[0] = om * (f0[j] - ext_k<T>(A, B, Cw, 0, ks)) + B.a[1];
+      o[1] = om * (f1[j] - ext_k<T>(A, B, Cw, 1, ks)) + B.a[2];
+      T* p = vb_ + (long long)(y + 1) * x.ld;
+      if (cin1) {
+        typedef T v2 __attribute__((ext_vector_type(2)));
+        v2 v;
+        v[0] = o[0];
+        v[1] = o[1];
+        *reinterpret_cast<v2*>(p) = v;
+      } else if (cin0) {
+        p[0] = o[0];
+      }
+    }
+    A = B;
+    B = Cw;
+  };
+  ext_unroll(emit, std::make_integer_sequence<int, PER>{});
+}
+
+template <typename T, bool FIX65>
+__global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail_ext(TailArgs<T> a, ExtArgs<T> x) {
+  __shared__ __attribute__((aligned(16))) char smem[kTailLdsBytes];
+  const int tid = threadIdx.x;
+  const int Ht = FIX65 ? 65 : a.Ht, Wt = FIX65 ? 65 : a.Wt;
+  const int tot = tail_off(Ht, Wt, FIX65 ? 6 : a.nlev);
+  T* es = reinterpret_cast<T*>(smem);  // the fast path's two regions: corrections, right-hand sides
+  T* fs = es + tot;
+  const int wv = tid >> 6, lane = tid & 63;
+  ext_down<T>(a, x, fs, Ht, Wt, wv, lane);
+  __syncthreads();
+#ifdef FEA_TAIL_TRACE
+  int nph = 0;
+#define FEA_EXT_NPH , nph
+#else
+#define FEA_EXT_NPH
+#endif
+  if constexpr (FIX65) tail_fast<T, false, 65, 6, true>(a, es, fs, nullptr, nullptr, nullptr, nullptr, wv, lane FEA_EXT_NPH);
+  else tail_fast<T, false, 0, 0, true>(a, es, fs, nullptr, nullptr, nullptr, nullptr, wv, lane FEA_EXT_NPH);
+#undef FEA_EXT_NPH
+  __syncthreads();
+  ext_up<T>(a, x, es, Ht, Wt, wv, lane);
+}
+
 }  // namespace fea
 
 using namespace fea;
@@ -694,6 +939,28 @@ static inline bool tail_dim_ok(int n, int nlev) {
 
 FEA_TAIL_API(f32, float)
 FEA_TAIL_API(f64, double)
+
+#define FEA_TAIL_EXT_API(SUF, T)                                                                              \
+  extern "C" int fea_mg_coarse_tail_ext_##SUF(const T* f_x, T* v_x, int Hx, int Wx, int ld_x, long long bs_x,  \
+                                              int nlev, const T* ktab, const T* omd, int ntab, const T* rtab,   \
+                                              const T* ptab, T w0, T w1, int B, void* stream) {                \
+    if (!f_x || !v_x || !ktab || !omd || !rtab || !ptab || B <= 0 || nlev < 1 || nlev > kTailMaxLevels)       \
+      return FEA_EINVAL;                                                                                      \
+    if (ntab != 1 || Hx < 5 || Wx < 5 || !(Hx & 1) || !(Wx & 1)) return FEA_EINVAL;                            \
+    const int Ht = (Hx + 1) / 2, Wt = (Wx + 1) / 2;                                                           \
+    if (!tail_dim_ok(Ht, nlev) || !tail_dim_ok(Wt, nlev)) return FEA_EINVAL;                                  \
+    if (ld_x < Wx + 128 / (int)sizeof(T) || bs_x < (long long)(Hx + 2) * ld_x) return FEA_EINVAL;              \
+    if (tail_lds_bytes<T>(Ht, Wt, nlev, false) > kTailLdsBytes) return FEA_EINVAL;                            \
+    TailArgs<T> a{f_x, v_x, nullptr, ktab, omd, rtab, ptab, w0, w1, Ht, Wt, nlev, ld_x, bs_x, 1, 1, 1, 0};       \
+    ExtArgs<T> x{f_x, v_x, Hx, Wx, ld_x, bs_x};                                                               \
+    hipStream_t s_ = (hipStream_t)stream;                                                                     \
+    if (Ht == 65 && Wt == 65 && nlev == 6) k_mg_coarse_tail_ext<T, true><<<B, kTailThreads, 0, s_>>>(a, x);     \
+    else k_mg_coarse_tail_ext<T, false><<<B, kTailThreads, 0, s_>>>(a, x);                                    \
+    FEA_LAUNCH_CHECK();                                                                                       \
+  }
+
+FEA_TAIL_EXT_API(f32, float)
+FEA_TAIL_EXT_API(f64, double)
 
 #ifdef FEA_TAIL_TRACE
 extern "C" int fea_tail_trace_read(long long* host) {

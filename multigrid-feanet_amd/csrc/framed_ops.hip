@@ -268,6 +268,7 @@ struct MgArgs {
   int clo, chi;      // column range of the residual norm
   int nt;            // 1: nontemporal stores (level larger than FEANET_NT_BYTES); 2: also loads (sweep, join)
   int rev;           // decode_task_lin: deal the launch's tasks in reverse order (last task first)
+  int flip;          // cycle join: every task streams in the other direction (even tasks bottom-up, odd top-down)
   // cycle join over up to 4 rectangles (nrect > 0; a domain-decomposed rank's border strips, then its interior):
   // rectangle r = coarse rows [rI0[r], rI1[r]) x fine columns [rc0[r], rc1[r]) (odd bounds, coarse column J owned
   // with its fine columns 2J-1, 2J), its nstrips rns[r], its row tasks rnt[r]; the launch's tasks per sample are
@@ -2326,6 +2327,8 @@ constexpr bool kJoinAlternate = FEA_JOIN_ALT != 0;
 // measured slower (+1.5 us per V-cycle, profiles/r05_ab/join_omz.txt)
 #ifdef FEA_LAB_JREV
 #define FEA_LAB_JOIN_REV(g) { static int flip = 0; (g).rev = flip = !flip; }
+#elif defined(FEA_LAB_JFLIP)
+#define FEA_LAB_JOIN_REV(g) { static int fl = 0; (g).flip = fl; fl ^= 1; }
 #else
 #define FEA_LAB_JOIN_REV(g)
 #endif
@@ -2733,7 +2736,7 @@ void k_mg_cycle_join(MgArgs<T> g) {
     const int cs = jt.c0 - Ovl3<T>::HL;
     const bool inner = kJoinInner && g.nrect == 0 && 2 * jt.I0 - 4 >= 1 && 2 * jt.I1 + 2 <= g.H - 2 && cs >= 1 &&
                        cs + kWave * Frame<T>::VEC - 1 <= g.W - 2;
-    if (kJoinAlternate && (jt.t & 1)) {
+    if ((kJoinAlternate && (jt.t & 1)) != (g.flip != 0)) {
       if (inner) join_task<T, MULTI, NT, NORM, true, NTF, false>(g, jt, tab, rtb, ptb, ssq);
       else join_task<T, MULTI, NT, NORM, true, NTF, true>(g, jt, tab, rtb, ptb, ssq);
     } else {

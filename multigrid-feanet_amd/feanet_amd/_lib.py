@@ -58,6 +58,7 @@ _SIGS = {
     "mg_hsweep_restrict": [P, P, P, P, P, P, P, P, I, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_prolong_hsweep": [P, P, P, P, P, P, P, P, P, I, P, I, P, I, "S", I, I, I, I, LL, I, LL, P],
     "mg_coarse_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, "S", "S", I, I, I, I, P],
+    "mg_coarse_tail_ext": [P, P, I, I, I, LL, I, P, P, I, P, P, "S", "S", I, P],
     "mg_hjac_tail": [P, P, I, I, I, I, LL, P, P, P, I, P, P, P, I, "S", "S", I, I, I, P],
     # several coarse levels per launch (pointer arrays: ptr_array())
     "mg_mid_down": [P, P, I, I, I, I, P, P, I, P, I, "S", I, I, P],

@@ -22,6 +22,9 @@ Steps:
   ("mid_up", a, k, csrc, dst, T)       the "omdf" prolong_sweep steps of levels a+k-1..a in one
                                        launch: u_a[dst] from u_{a+k}[csrc] (tile T of level a)
                                        (group_mid rewrites a schedule into these)
+  ("coarse_tail_ext", l, dst)          the zero-guess restriction of level l, the coarse tail of levels
+                                       l+1..L-1 and level l's recomputed-iterate prolongation + sweep in one
+                                       launch (fea_mg_coarse_tail_ext; extend_tail rewrites into it)
 
 Semantics reproduced:
   * nu1 = nu2 = 1: MultiGrid.Step (M-FEANet-mg_test.ipynb:27346-27372) == MultiGrid.iterate
@@ -342,6 +345,27 @@ def group_mid(steps, pick_down, pick_up):
                     out.append(run[m])
                     m += 1
             i = j + 1
+            continue
+        out.append(st)
+        i += 1
+    return out
+
+
+def extend_tail(steps):
+    """Rewrite ("resid_restrict", l, None, None), ("coarse_tail", l+1, c), ("prolong_sweep", l, OMDF, c, dst) — the
+    level right above the coarse tail going down into it and back up — into ONE ("coarse_tail_ext", l, dst) step
+    (fea_mg_coarse_tail_ext, bitwise the three launches).  Run after pair_restrictions / pair_prolongations: only a
+    level they left to single-level launches has that shape."""
+    out = []
+    i = 0
+    while i < len(steps):
+        st = steps[i]
+        if (i + 2 < len(steps) and st[0] == "resid_restrict" and st[2] is None and st[3] is None
+                and steps[i + 1][0] == "coarse_tail" and steps[i + 1][1] == st[1] + 1
+                and steps[i + 2][0] == "prolong_sweep" and steps[i + 2][1] == st[1] and steps[i + 2][2] == OMDF
+                and steps[i + 2][3] == steps[i + 1][2]):
+            out.append(("coarse_tail_ext", st[1], steps[i + 2][4]))
+            i += 3
             continue
         out.append(st)
         i += 1

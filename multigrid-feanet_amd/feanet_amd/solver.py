@@ -25,7 +25,8 @@ import numpy as np
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import OMDF, group_hmid, group_mid, hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
+from .schedule import (OMDF, extend_tail, group_hmid, group_mid, hjac_schedule, pair_prolongations, pair_restrictions,
+                       vcycle_schedule)
 
 
 _SOLVERS = weakref.WeakValueDictionary()  # handle -> live MultigridSolver (torch.ops.feanet.mg_step)
@@ -136,6 +137,11 @@ class MultigridSolver:
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
     HMID_NODES = 300000   # learned-smoother levels paired into the HJac two-level launches: <= 513^2 nodes
     HMID_MIN_TILES = 64   # workgroups an HJac two-level launch should give the CUs (one per CU: LDS)
+    TAIL_EXT = True       # the single-level restriction / prolongation right above the coarse tail run inside the
+    TAIL_EXT_MIN_BATCH = 64  # tail's launch (fea_mg_coarse_tail_ext: single pattern, V(1,1)) for batches of at least
+    #                       this many samples: one workgroup per sample moves the level's traffic through one CU, which
+    #                       only pays when the samples fill the chip (C5, 256 x 1025^2 fp32: 1142 -> 1125 us; at B = 1
+    #                       the metric cycle 130.1 -> 134.1 us, C2 33.8 -> 37.6; profiles/r06_ab/tail_ext.txt)
 
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
@@ -429,7 +435,15 @@ class MultigridSolver:
             if self.pair_levels:
                 ok = lambda l: l + 2 < self.L and self.levels[l + 2].H >= 3 and self.levels[l + 2].W >= 3
                 steps = pair_prolongations(pair_restrictions(steps, ok), ok)
+            if self._tail_ext_ok():
+                steps = extend_tail(steps)
         return [self.bind_step(st) for st in steps], end
+
+    def _tail_ext_ok(self):
+        """fea_mg_coarse_tail_ext's scope: the single-pattern V(1,1) tail, the level above it at most 129 wide."""
+        t = self.tail_from
+        return (self.TAIL_EXT and t is not None and self.B >= self.TAIL_EXT_MIN_BATCH and self.ntab == 1
+                and self.nu1 == 1 and self.nu2 == 1 and self.compat is None and self.levels[t - 1].W <= 129 and self.levels[t - 1].H <= 129)
 
     def _mid_tile(self, up, a, k):
         """Tile size for a multi-level launch over levels a..a+k-1 (down: tile of level a+k; up: of
@@ -569,6 +583,10 @@ class MultigridSolver:
                                        lv[t].bs, None if self.tail_pid is None else self.tail_pid.data_ptr(),
                                        kt, om, nt, rt, pt, self.w[0], self.w[1], self.nu1, self.nu2,
                                        int(self.compat == "mm_interface_q2"), lv[t].B))
+        if kind == "coarse_tail_ext":
+            x, t = l, l + 1
+            return ("mg_coarse_tail_ext", (f, ptr(x, st[2]), lv[x].H, lv[x].W, lv[x].ld, lv[x].bs, self.L - t, kt, om,
+                                           nt, rt, pt, self.w[0], self.w[1], lv[x].B))
         if kind == "hsweep_restrict":
             return ("mg_hsweep_restrict", (ptr(l, st[2]), None, f, ptr(l, st[3]), lv[l + 1].f.data_ptr(), pid(l), kt,
                                            om, nt, self.hw.data_ptr(), self.nl, rt, nr, self.w[0]) + geom(l) +
@@ -1048,6 +1066,10 @@ class MultigridSolver:
         total = 0
         for name, args in plan:
             if name in ("mg_coarse_tail", "mg_hjac_tail"):
+                continue
+            if name == "mg_coarse_tail_ext":  # read f_X twice (down, up), write v_X (the tail itself: LDS)
+                H, W, B = args[2], args[3], args[-1]
+                total += 3 * esz * B * (H - 2) * (W - 2)
                 continue
             if name == "mg_hsweep":  # read u (NULL: zero guess) and f (+ pattern), write out
                 B, H, W = args[-5:-2]

@@ -1233,3 +1233,74 @@ def test_cycle_join_rects_bitwise(T, m, n, B, problem, cut):
         got_u, got_f = run(sets)
         assert torch.equal(got_u, ref_u), (sets, (got_u - ref_u).abs().max().item())
         assert np.array_equal(got_f, ref_f), sets
+
+
+@pytest.mark.parametrize("T", [torch.float32, torch.float64])
+@pytest.mark.parametrize("n,m,nlev,B", [(128, None, 6, 1), (128, None, 6, 3), (128, None, 2, 2), (64, None, 5, 1),
+                                        (16, None, 3, 2), (8, None, 2, 1), (128, 64, 2, 1), (64, 128, 3, 2)])
+def test_coarse_tail_ext_bitwise(T, n, m, nlev, B):
+    """fea_mg_coarse_tail_ext (the level X above the coarse tail restricted into the tail's LDS and prolonged back out
+    of it inside the tail's launch) is bitwise the three launches it replaces: the zero-guess
+    fea_mg_residual_restrict of X, fea_mg_coarse_tail on the next level, fea_mg_prolong_sweep(u = NULL) of X — at the
+    65^2 / 6-level tail of every BASELINE plan (129^2 X) and the general tails (smaller, rows != columns), batches;
+    X's boundary nodes are left untouched."""
+    from feanet_amd import _lib
+    rng = np.random.default_rng(29 * n + B)
+    m_ = n if m is None else m
+    X = Frame(n, B, T, "poisson", m=m)
+    t = Frame(n // 2, B, T, "poisson", m=m_ // 2)
+    ktab, omd, R, P, kt, om, rt, pt = tables("poisson", T)
+    _, f = rand_state(rng, B, (X.H, X.W), T)
+    X.put("f", f)
+    sentinel = np.full((B, X.H, X.W), 7.0)
+    X.put("a", sentinel)
+    X.put("b", sentinel)
+    w0, w1 = 1.25, 0.75
+    _lib.call("mg_residual_restrict", T, None, X.L.f.data_ptr(), None, t.L.f.data_ptr(), None, kt.data_ptr(),
+              om.data_ptr(), 1, rt.data_ptr(), 1, w0, *X.args(), t.L.ld, t.L.bs, None)
+    _lib.call("mg_coarse_tail", T, t.L.f.data_ptr(), t.L.a.data_ptr(), t.H, t.W, nlev, t.L.ld, t.L.bs, None,
+              kt.data_ptr(), om.data_ptr(), 1, rt.data_ptr(), pt.data_ptr(), w0, w1, 1, 1, 0, B, None)
+    _lib.call("mg_prolong_sweep", T, None, t.L.a.data_ptr(), X.L.f.data_ptr(), X.L.a.data_ptr(), None, None,
+              kt.data_ptr(), om.data_ptr(), 1, pt.data_ptr(), 1, w1, *X.args(), t.L.ld, t.L.bs, None)
+    ref = X.get("a")
+    _lib.call("mg_coarse_tail_ext", T, X.L.f.data_ptr(), X.L.b.data_ptr(), X.H, X.W, X.L.ld, X.L.bs, nlev,
+              kt.data_ptr(), om.data_ptr(), 1, rt.data_ptr(), pt.data_ptr(), w0, w1, B, None)
+    got = X.get("b")
+    assert np.array_equal(got, ref), f"{np.argwhere(got != ref)[:5]}"
+    assert (got[:, 0, :] == 7).all() and (got[:, -1, :] == 7).all() and (got[:, :, 0] == 7).all()
+    assert (got[:, :, -1] == 7).all()
+
+
+@pytest.mark.parametrize("T,n,B", [(torch.float64, 4096, 1), (torch.float64, 1024, 1), (torch.float32, 1024, 4),
+                                   (torch.float64, 256, 2)])
+def test_solver_tail_ext(T, n, B):
+    """The solver's plan runs the level above the 65^2 tail inside the tail's launch (fea_mg_coarse_tail_ext) where
+    the level pairing leaves it alone (4097^2: levels 1-2 and 3-4 paired, the 129^2 level 5 extended; 1025^2:
+    levels 1-2 paired, level 3), and single / joined V-cycles with and without it are bitwise the same.  (By default
+    only batches >= TAIL_EXT_MIN_BATCH take it; forced on here.)"""
+    from feanet_amd.solver import MultigridSolver
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    f = torch.randn(B, 1, n + 1, n + 1, dtype=T, device="cuda", generator=g)
+    outs = []
+    for ext in (True, False):
+        s = MultigridSolver(n, dtype=T, batch=B)
+        s.TAIL_EXT, s.TAIL_EXT_MIN_BATCH = ext, 1
+        names = [nm for nm, _ in s._plan("a")[0]]
+        assert ("mg_coarse_tail_ext" in names) == ext and ("mg_coarse_tail" in names) != ext, names
+        s.set_rhs(f=f)
+        s.load()
+        s.vcycle(1)
+        one = s.solution()
+        s.vcycle(5)
+        outs.append((one, s.solution()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_solver_tail_ext_default_by_batch():
+    """TAIL_EXT_MIN_BATCH: the batch-1 plan keeps the streaming launches around the tail, a 64-sample plan extends it."""
+    from feanet_amd.solver import MultigridSolver
+    for B, ext in ((1, False), (64, True)):
+        s = MultigridSolver(256, dtype=torch.float32, batch=B)
+        names = [nm for nm, _ in s._plan("a")[0]]
+        assert ("mg_coarse_tail_ext" in names) == ext, (B, names)

@@ -38,6 +38,9 @@ def interpret(mg, steps, v, f, compat=None):
             expanded += [("resid_restrict", st[1], None, None), ("resid_restrict", st[1] + 1, None, None)]
         elif st[0] == "prolong_sweep2":  # feanet_amd.schedule.pair_prolongations
             expanded += [("prolong_sweep", st[1] + 1, "omdf", st[2], "mid"), ("prolong_sweep", st[1], "omdf", "mid", st[3])]
+        elif st[0] == "coarse_tail_ext":  # feanet_amd.schedule.extend_tail
+            expanded += [("resid_restrict", st[1], None, None), ("coarse_tail", st[1] + 1, "ext"),
+                         ("prolong_sweep", st[1], "omdf", "ext", st[2])]
         elif st[0] == "hmid_down":  # feanet_amd.schedule.group_hmid
             expanded += [("hsweep_restrict", st[1], None, st[2]), ("hsweep_restrict", st[1] + 1, None, st[3])]
         elif st[0] == "hmid_up":
@@ -394,3 +397,28 @@ def test_vcycle_blocks_cover_k(k):
     assert sum(b != G for b in pb) <= 1 and (pb[-1] == k % G if k % G else pb[-1] == G)
     gb = MultigridSolver.graph_blocks(k, G)
     assert sum(gb) == k and all(b & (b - 1) == 0 for b in gb)
+
+
+@pytest.mark.parametrize("problem", ["poisson", "interface"])
+@pytest.mark.parametrize("L,tail", [(6, 5), (6, 4), (5, 2), (6, 3)])
+def test_extend_tail_equals_per_level(problem, L, tail):
+    """extend_tail (fea_mg_coarse_tail_ext: the level right above the coarse tail restricted into it and prolonged
+    out of it in the tail's launch) after the level pairing: only a level the pairing left alone is absorbed (an odd
+    number of zero-guess restrictions above the tail), and the rewritten schedule is the per-level V-cycle."""
+    from feanet_amd.schedule import extend_tail, pair_prolongations, pair_restrictions
+    n = 64
+    rng = np.random.default_rng(23)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L)
+    mg.nu, mg.q2 = (1, 1), False
+    v = rng.standard_normal((2, n + 1, n + 1))
+    f = rng.standard_normal((2, n + 1, n + 1))
+    steps, end = vcycle_schedule(L, 1, 1, tail_from=tail)
+    ok = lambda l: l + 2 < L
+    paired = pair_prolongations(pair_restrictions(steps, ok), ok)
+    ext = extend_tail(paired)
+    kinds = [s_[0] for s_ in ext]
+    assert kinds.count("coarse_tail_ext") == (1 if (tail - 1) % 2 == 1 else 0), ext
+    assert kinds.count("coarse_tail") + kinds.count("coarse_tail_ext") == 1
+    ref = interpret(mg, steps, v, f)[0][end]
+    np.testing.assert_array_equal(interpret(mg, ext, v, f)[0][end], ref)
+    assert extend_tail(steps) != steps or tail == 1  # unpaired schedule: the level above the tail is always alone

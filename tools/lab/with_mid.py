@@ -14,7 +14,8 @@ from feanet_amd.solver import MultigridSolver  # noqa: E402
 for kv in sys.argv[1].split(","):
     if kv and kv != "-":
         k, v = kv.split("=")
-        setattr(MultigridSolver, k, type(getattr(MultigridSolver, k))(v))
+        old = getattr(MultigridSolver, k)
+        setattr(MultigridSolver, k, v not in ("0", "False", "false") if isinstance(old, bool) else type(old)(v))
 sys.argv = sys.argv[2:]
 sys.path.insert(0, os.path.dirname(os.path.abspath(sys.argv[0])))
 runpy.run_path(sys.argv[0], run_name="__main__")
