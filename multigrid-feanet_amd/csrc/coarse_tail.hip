@@ -17,7 +17,12 @@
 
 namespace fea {
 
-constexpr int kTailThreads = 1024;
+// threads per tail workgroup (one per sample; waves split each level's rows).  FEA_TAIL_THREADS: lab builds
+#ifndef FEA_TAIL_THREADS
+#define FEA_TAIL_THREADS 1024
+#endif
+constexpr int kTailThreads = FEA_TAIL_THREADS;
+static_assert(kTailThreads % 64 == 0 && kTailThreads >= 256 && kTailThreads <= 1024, "tail: 4..16 waves");
 constexpr int kTailMaxLevels = 8;
 constexpr int kTailMaxN = 65;  // per dimension
 constexpr int kTailLdsBytes = 160 * 1024 - 1024;
@@ -89,8 +94,10 @@ __device__ __forceinline__ int tail_off(int Ht, int Wt, int k) {  // element off
 // Every node value is the same expression, in the same order, as the general path (bitwise):
 // acc chains start from 0 and add the taps in (row, column) order; x = fma(w1, P e, omd f).
 // ---------------------------------------------------------------------------------------------
-constexpr int kTailDownRows = 2;  // coarse rows per wave going down: Hc - 2 <= 31 over 16 waves
-constexpr int kTailUpRows = 4;    // fine rows per wave going up / at the coarsest level: H - 2 <= 63
+constexpr int kTailDownRows = (31 + kTailThreads / 64 - 1) / (kTailThreads / 64);  // coarse rows per wave going down:
+//                                                                                   Hc - 2 <= 31 (2 over 16 waves)
+constexpr int kTailUpRows = (63 + kTailThreads / 64 - 1) / (kTailThreads / 64);  // fine rows per wave going up / at the
+//                                                                                 coarsest level: H - 2 <= 63 (4)
 // FEA_TAIL_LATE_SYNC: the two-material 65^2 tail takes its staging barrier inside the first phase (down_rows SYNC)
 #ifndef FEA_TAIL_LATE_SYNC
 #define FEA_TAIL_LATE_SYNC 1
@@ -540,10 +547,11 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
       }
     return acc;
   };
-  // threads as a 32 x 32 grid over the interior nodes (no per-node integer division)
+  // threads as a 32 x (threads / 32) grid over the interior nodes (no per-node integer division)
+  constexpr int kTy = kTailThreads / 32;
   const int tx = tid & 31, ty = tid >> 5;
   auto sweep = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst, bool zero) {
-    for (int r = 1 + ty; r <= H - 2; r += 32)
+    for (int r = 1 + ty; r <= H - 2; r += kTy)
       for (int c = 1 + tx; c <= N - 2; c += 32) {
         const int i = r * N + c;
         const T om = ktb[P(pk, i) + 9];
@@ -552,13 +560,13 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
     FEA_TAIL_SYNC();
   };
   auto residual = [&](int H, int N, const uint8_t* pk, const T* f, const T* src, T* dst) {
-    for (int r = 1 + ty; r <= H - 2; r += 32)
+    for (int r = 1 + ty; r <= H - 2; r += kTy)
       for (int c = 1 + tx; c <= N - 2; c += 32) dst[r * N + c] = f[r * N + c] - Ku(N, pk, src, r, c);
     FEA_TAIL_SYNC();
   };
   auto restrict_ = [&](int H, int N, const uint8_t* pk, const T* res, T* fc) {  // fine residual -> coarse f
     const int Nc = (N + 1) / 2, Hc = (H + 1) / 2;
-    for (int I = 1 + ty; I <= Hc - 2; I += 32)
+    for (int I = 1 + ty; I <= Hc - 2; I += kTy)
       for (int J = 1 + tx; J <= Nc - 2; J += 32) {
       T acc = 0;
 #pragma unroll
@@ -574,7 +582,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_coarse_tail(TailArgs<T> a) 
   };
   auto prolong_add = [&](int H, int N, const uint8_t* pkc, T* v, const T* e) {  // v += w1 P e, interior
     const int Nc = (N + 1) / 2;
-    for (int y = 1 + ty; y <= H - 2; y += 32)
+    for (int y = 1 + ty; y <= H - 2; y += kTy)
       for (int x = 1 + tx; x <= N - 2; x += 32) {
       T acc = 0;
 #pragma unroll
@@ -720,7 +728,7 @@ __device__ __forceinline__ void ext_load(const T* p, T& x0, T& x1) {
 template <typename T>
 __device__ __forceinline__ void ext_down(const TailArgs<T>& a, const ExtArgs<T>& x, T* fs0, int Ht, int Wt, int wv,
                                          int lane) {
-  constexpr int PER = 4, R = 2 * PER + 3;  // Ht - 2 <= 63 coarse rows over 16 waves
+  constexpr int PER = (63 + kTailThreads / 64 - 1) / (kTailThreads / 64), R = 2 * PER + 3;  // Ht - 2 <= 63 coarse rows
   constexpr int NW = kTailThreads / 64;
   const int per = (Ht - 2 + NW - 1) / NW;
   const int I0 = 1 + wv * per, I1 = min(Ht - 1, I0 + per);
@@ -786,7 +794,7 @@ __device__ __forceinline__ void ext_down(const TailArgs<T>& a, const ExtArgs<T>&
 template <typename T>
 __device__ __forceinline__ void ext_up(const TailArgs<T>& a, const ExtArgs<T>& x, const T* es0, int Ht, int Wt, int wv,
                                        int lane) {
-  constexpr int PER = 8, R = PER + 2;  // x rows y0-1 .. y0+PER
+  constexpr int PER = 2 * ((127 + kTailThreads / 32 - 1) / (kTailThreads / 32)), R = PER + 2;  // x rows y0-1 .. y0+PER
   constexpr int NW = kTailThreads / 64;
   const int H = x.H, W = x.W;
   const int per = 2 * ((H - 2 + 2 * NW - 1) / (2 * NW));  // even: y0 - 1 is even on every wave

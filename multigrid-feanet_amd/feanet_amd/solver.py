@@ -137,6 +137,7 @@ class MultigridSolver:
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
     HMID_NODES = 300000   # learned-smoother levels paired into the HJac two-level launches: <= 513^2 nodes
     HMID_MIN_TILES = 64   # workgroups an HJac two-level launch should give the CUs (one per CU: LDS)
+    TAIL_MAX_N = 65       # the coarse tail (one LDS-resident launch) covers the levels of at most this many rows / columns
     TAIL_EXT = True       # the single-level restriction / prolongation right above the coarse tail run inside the
     TAIL_EXT_MIN_BATCH = 64  # tail's launch (fea_mg_coarse_tail_ext: single pattern, V(1,1)) for batches of at least
     #                       this many samples: one workgroup per sample moves the level's traffic through one CU, which
@@ -236,7 +237,7 @@ class MultigridSolver:
             esz = 4 if dtype == torch.float32 else 8
             for l in range(1, self.L):
                 Lv = self.levels[l]
-                if (Lv.H <= 65 and Lv.W <= 65
+                if (Lv.H <= self.TAIL_MAX_N and Lv.W <= self.TAIL_MAX_N
                         and 0 < _lib.coarse_tail_lds_bytes(Lv.H, Lv.W, self.L - l, esz, multi) <= _lib.TAIL_LDS_LIMIT):
                     self.tail_from = l
                     break
