@@ -32,6 +32,7 @@ import argparse
 import contextlib
 import faulthandler
 import json
+import math
 import os
 import sys
 import threading
@@ -515,6 +516,31 @@ def time_steps(s, steps, warmup, ws):
     return max_over_ranks(time.perf_counter() - t0, ws), calls * steps
 
 
+def time_to_solution(conv, ms_step, eps=1e-6):
+    """Cycles (and microseconds at the measured rate) to cut the residual by `eps` from the zero guess, at the
+    contraction factor measured over the first 8 cycles."""
+    if not (0.0 < conv < 1.0):
+        return None
+    cyc = math.ceil(math.log(eps) / math.log(conv))
+    return {"eps": eps, "contraction": conv, "cycles": cyc, "us": cyc * ms_step * 1e3,
+            "note": "cycles = ceil(log(eps) / log(contraction)), contraction over the first 8 cycles from zero"}
+
+
+def jacobi_same_grid(args, B, T, f):
+    """MG-Jacobi (the default V(1,1)) on the grid and right-hand side of a --smoother hjac line: its per-cycle time
+    (vcycle(K) with K = min(steps, 200), after the same warm-up) and time to 1e-6, beside the learned smoother's."""
+    from feanet_amd.solver import MultigridSolver
+    s = MultigridSolver(args.n, problem=args.problem, dtype=T, batch=B, levels=args.levels)
+    s.set_rhs(f=f)
+    s.load()
+    conv = contraction(s)
+    k = max(1, min(args.steps, 200))
+    t, _ = time_steps(s, k, args.warmup, 1)
+    ms = t / k * 1e3
+    del s
+    return {"ms_per_step": ms, "time_to_solution": time_to_solution(conv, ms), "steps": k}
+
+
 def contraction(s):
     """Residual contraction factor per cycle over the first 8 cycles from zero (before the fp64 floor)."""
     s.load()
@@ -751,7 +777,13 @@ def run_single(args, ws, rank, T, B):
     vbytes = s.bytes_per_vcycle(args.steps)
     rec.update({"roofline": roof, "north_star_kernel": ns, "fine_level_kernels": fl,
                 "vcycle_hbm_gbps_algorithmic": vbytes / (t / args.steps) / 1e9 if (ws == 1 and vbytes) else None,
-                "vcycle_algorithmic_bytes": vbytes, "residual_contraction_per_cycle": conv})
+                "vcycle_algorithmic_bytes": vbytes, "residual_contraction_per_cycle": conv,
+                "time_to_solution": time_to_solution(conv, ms_step)})
+    if args.smoother == "hjac" and ws == 1 and B == 1:
+        f = s.levels[0].view(s.levels[0].f).clone().reshape(B, 1, N, N)
+        del s
+        torch.cuda.empty_cache()
+        rec["jacobi_same_grid"] = jacobi_same_grid(args, B, T, f)
     if args.problem == "interface":
         rec["config"]["transfer"] = ("learned ratio R/P/w (feanet_amd/weights/multigrid_interface_ratio.npz)" if learned
                                      else "linear (the reference's default RestrictionNet / ProlongationNet)")
