@@ -27,6 +27,9 @@ constexpr int kTailMaxLevels = 8;
 constexpr int kTailMaxN = 65;  // per dimension
 constexpr int kTailLdsBytes = 160 * 1024 - 1024;
 constexpr int kTS = 10;  // table stride (9 weights + omega/d)
+#ifndef FEA_KSYM  // two-material K from the centre's table row (see framed_ops.hip kapply)
+#define FEA_KSYM 1
+#endif
 
 #ifdef FEA_TAIL_TRACE  // lab builds only (tools/lab/tail_lab.py): a timestamp after every barrier
 __device__ long long g_tail_trace[256];
@@ -160,6 +163,15 @@ struct TailFast {
   __device__ __forceinline__ T Kx(int j, const T (&xl)[R], const T (&x)[R], const T (&xr)[R], const int (&ql)[R],
                                   const int (&q)[R], const int (&qr)[R]) const {
     T acc = 0;
+    if constexpr (MULTI && FEA_KSYM) {  // the centre's table row, mirrored taps (framed_ops.hip kapply): same bits
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        acc += kw(q[j], 8 - dr * 3) * xl[j - 1 + dr];
+        acc += kw(q[j], 7 - dr * 3) * x[j - 1 + dr];
+        acc += kw(q[j], 6 - dr * 3) * xr[j - 1 + dr];
+      }
+      return acc;
+    }
 #pragma unroll
     for (int dr = 0; dr < 3; ++dr) {
       acc += kw(ql[j - 1 + dr], dr * 3 + 0) * xl[j - 1 + dr];

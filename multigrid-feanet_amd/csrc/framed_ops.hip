@@ -208,12 +208,32 @@ __device__ __forceinline__ PRow<V> finish_p(const RawP<V>& r) {
 }
 
 // (K u) at own column k (k = 0..V, k = V is the R column) from the 3-row window.
+// Two-material (MULTI): KNet applies tap t with the weight of the NEIGHBOUR's pattern (split, then convolve:
+// FEANet/model.py:22-30); K is a symmetric FE stiffness, so that weight is bit for bit the mirrored tap 8 - t of the
+// CENTRE's pattern (stencil_table(); MultigridSolver checks it on every level's map, mesh_setup
+// .stencil_mirror_mismatches).  All nine weights then come from one table row — one base address, adjacent
+// offsets — instead of three rows picked by the window's neighbour patterns; taps are summed in the same order, so
+// every value is the same bits as before.
+#ifndef FEA_KSYM
+#define FEA_KSYM 1
+#endif
 template <typename T, int V, bool MULTI>
 __device__ __forceinline__ T kapply(const Row<T, V>& w0, const Row<T, V>& w1, const Row<T, V>& w2,
                                     const PRow<V>& p0, const PRow<V>& p1, const PRow<V>& p2, int k,
                                     const T (&ks)[9], const T* tab) {
   T acc;
-  if constexpr (!MULTI) {
+  if constexpr (MULTI && FEA_KSYM) {
+    const int pc = p1.a[k + 1];
+    acc = tabv(tab, pc, 8) * w0.a[k];
+    acc += tabv(tab, pc, 7) * w0.a[k + 1];
+    acc += tabv(tab, pc, 6) * w0.a[k + 2];
+    acc += tabv(tab, pc, 5) * w1.a[k];
+    acc += tabv(tab, pc, 4) * w1.a[k + 1];
+    acc += tabv(tab, pc, 3) * w1.a[k + 2];
+    acc += tabv(tab, pc, 2) * w2.a[k];
+    acc += tabv(tab, pc, 1) * w2.a[k + 1];
+    acc += tabv(tab, pc, 0) * w2.a[k + 2];
+  } else if constexpr (!MULTI) {
     acc = ks[0] * w0.a[k];
     acc += ks[1] * w0.a[k + 1];
     acc += ks[2] * w0.a[k + 2];

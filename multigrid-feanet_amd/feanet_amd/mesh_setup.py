@@ -125,3 +125,26 @@ def interface_pattern_map_device(N, shape=0, size=2.0, device="cuda", out=None, 
     if rc != 0:
         raise RuntimeError(f"feanet_amd: fea_interface_pattern_map failed ({rc})")
     return out
+
+
+def stencil_mirror_mismatches(ktab, pid):
+    """Interior (node, tap) pairs where the stiffness weight of tap t taken from the NEIGHBOUR's pattern (KNet's
+    split-then-convolve order, FEANet/model.py:22-30) differs from the mirrored tap 8 - t of the CENTRE's pattern.
+    K is a symmetric FE stiffness (K_ij = K_ji), so for the tables of stencil_table() this is 0 bit for bit on any
+    pattern map; the framed two-material kernels rely on it (one table row per node).  ktab: [P, 9] or [P, 3, 3];
+    pid: [H, W] pattern ids (numpy or torch, any device)."""
+    import torch
+    p = pid if torch.is_tensor(pid) else torch.from_numpy(np.ascontiguousarray(pid))
+    k = torch.as_tensor(np.asarray(ktab, np.float32).reshape(-1, 9) if not torch.is_tensor(ktab) else ktab.reshape(-1, 9),
+                        device=p.device)
+    p = p.long()
+    H, W = p.shape
+    if H < 3 or W < 3:
+        return 0
+    c = p[1:-1, 1:-1]
+    bad = 0
+    for t in range(9):
+        dy, dx = t // 3 - 1, t % 3 - 1
+        nb = p[1 + dy:H - 1 + dy, 1 + dx:W - 1 + dx]
+        bad += int((k[nb, t] != k[c, 8 - t]).sum().item())
+    return bad

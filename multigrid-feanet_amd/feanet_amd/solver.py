@@ -232,6 +232,13 @@ class MultigridSolver:
             # two-material pattern maps: built on the device (setup_ops.hip), bit-identical to the host
             self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid_shape=(shape, size) if multi else None))
         self.fine_pid = ms.interface_pattern_map_device(n + 1, shape, size, device=dev) if multi else None
+        if multi:  # the framed kernels read each node's stiffness row from its own pattern (K symmetric; checked)
+            for Lv in self.levels:
+                off = 128 // (4 if dtype == torch.float32 else 8) - 1
+                pv = Lv.pid[:(Lv.H + 2) * Lv.ld].view(Lv.H + 2, Lv.ld)[1:Lv.H + 1, off:off + Lv.W]
+                if ms.stencil_mirror_mismatches(ktab, pv):
+                    raise ValueError("MultigridSolver: the stiffness table is not symmetric on this pattern map "
+                                     "(the framed two-material kernels need K_ij == K_ji bit for bit)")
         self.tail_from = None
         if coarse_tail:
             esz = 4 if dtype == torch.float32 else 8
