@@ -1,5 +1,6 @@
 """Product setup code (feanet_amd.mesh_setup: vectorised pattern maps, stencil/mass tables)
 against golden tables generated from the reference.  CPU only, bit-exact."""
+import pytest
 import numpy as np
 
 from feanet_amd import mesh_setup as ms
@@ -88,3 +89,17 @@ def test_vtk_export_roundtrip(tmp_path):
     d = read_vtk_legacy(str(q))
     assert (d["CELL_DATA"]["Phase"] == 0).all()
     np.testing.assert_array_equal(d["POINT_DATA"]["u"], u)
+
+
+@pytest.mark.parametrize("prop", [(1, 20), (1, 5), (3, 7)])
+@pytest.mark.parametrize("shape", [0, 1])
+def test_stiffness_mirror_symmetry(prop, shape):
+    """The framed two-material kernels take every node's nine stiffness weights from its own pattern's table row,
+    mirrored (tap 8 - t), where KNet weighs tap t by the neighbour's pattern (FEANet/model.py:22-30): equal bit for bit
+    because K is a symmetric FE stiffness — on every level map of both inclusion shapes; a random table is not."""
+    from feanet_amd import mesh_setup as ms
+    kt = ms.stencil_table(prop)
+    for N in (5, 9, 33, 65, 129, 257):
+        assert ms.stencil_mirror_mismatches(kt, ms.interface_pattern_map(N, shape, 2.0)) == 0, N
+    rng = np.random.default_rng(1)
+    assert ms.stencil_mirror_mismatches(rng.standard_normal((16, 9)), ms.interface_pattern_map(65, shape, 2.0)) > 0
