@@ -133,6 +133,8 @@ class MultigridSolver:
     #                       519, C3 92.0 -> 90.0, C5 level, DD 8-rank projection 108.9 -> 104.6 against 300000 (<= 513^2,
     #                       rounds 2-5), once this round's task heights had sped the two-level kernels up
     #                       (profiles/r06_ab/mid_nodes.txt).  Larger values still select the multi-level launches (bitwise).
+    MID_NODES_DOWN = None  # per-direction overrides of MID_NODES (None: MID_NODES)
+    MID_NODES_UP = None
     MID_MIN_TILES = 200   # workgroups a multi-level launch should give the 256 CUs
     MID_MAX_REDUNDANCY = 3.0  # staged top-level region / owned nodes (down pass)
     HMID_NODES = 300000   # learned-smoother levels paired into the HJac two-level launches: <= 513^2 nodes
@@ -509,7 +511,8 @@ class MultigridSolver:
 
     def _pick_mid(self, levels, up):
         """Groups (a, k, T) of consecutive latency-bound levels, formed from the coarse end upward."""
-        cap = self.MID_NODES
+        cap = self.MID_NODES_UP if up else self.MID_NODES_DOWN
+        cap = self.MID_NODES if cap is None else cap
         el = sorted(l for l in levels
                     if self.B * self.levels[l].H * self.levels[l].W <= cap and l + 1 < self.L)
         groups = []

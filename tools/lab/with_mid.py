@@ -15,7 +15,13 @@ for kv in sys.argv[1].split(","):
     if kv and kv != "-":
         k, v = kv.split("=")
         old = getattr(MultigridSolver, k)
-        setattr(MultigridSolver, k, v not in ("0", "False", "false") if isinstance(old, bool) else type(old)(v))
+        if isinstance(old, bool):
+            v = v not in ("0", "False", "false")
+        elif old is None:
+            v = int(v)
+        else:
+            v = type(old)(v)
+        setattr(MultigridSolver, k, v)
 sys.argv = sys.argv[2:]
 sys.path.insert(0, os.path.dirname(os.path.abspath(sys.argv[0])))
 runpy.run_path(sys.argv[0], run_name="__main__")
