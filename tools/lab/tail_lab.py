@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.join(HERE, "..", "..")
-SO = os.path.join(HERE, "tail_lab.so")
+SO = os.path.join(ROOT, "lab_libs", "tail_lab.so")  # (lab_libs/ travels to the GPU box; tools/lab/*.so does not)
 SRC = os.path.join(ROOT, "multigrid-feanet_amd", "csrc", "coarse_tail.hip")
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
@@ -39,9 +39,22 @@ B = int(os.environ.get("B", 1))  # B samples = B workgroups, one per CU (B = 256
 f = torch.randn(B * bs, dtype=T, device=dev)
 v = torch.zeros(B * bs, dtype=T, device=dev)
 buf = (ctypes.c_longlong * 256)()
+ntab, pidl = 1, None
+if os.environ.get("MULTI") == "1":  # the two-material tail: 16 stencils, per-level pattern maps (MeshCenterInterface)
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "multigrid-feanet_amd"))
+    from feanet_amd import mesh_setup as ms
+    kt = ms.stencil_table((1, 20))
+    ntab = kt.shape[0]
+    ktab = torch.from_numpy(kt.reshape(-1, 9).astype(np.float64)).to(dev)
+    omd = torch.from_numpy(ms.omega_over_d(kt, 2 / 3., np.float64)).to(dev)
+    rtab = lin.reshape(1, 9).expand(ntab, 9).contiguous().to(dev)
+    pidl = torch.from_numpy(np.concatenate([ms.interface_pattern_map(((Ht - 1) >> k) + 1).reshape(-1)
+                                            for k in range(nl)])).to(dev)
 for rep in range(3):
-    rc = L.fea_mg_coarse_tail_f64(f.data_ptr(), v.data_ptr(), Ht, Ht, nl, ld, bs, None, ktab.data_ptr(),
-                                  omd.data_ptr(), 1, rtab.data_ptr(), rtab.data_ptr(), 1.0, 1.0, 1, 1, 0, B, s)
+    rc = L.fea_mg_coarse_tail_f64(f.data_ptr(), v.data_ptr(), Ht, Ht, nl, ld, bs,
+                                  None if pidl is None else pidl.data_ptr(), ktab.data_ptr(),
+                                  omd.data_ptr(), ntab, rtab.data_ptr(), rtab.data_ptr(), 1.0, 1.0, 1, 1, 0, B, s)
     assert rc == 0, rc
     torch.cuda.synchronize()
 L.fea_tail_trace_read(buf)
@@ -53,5 +66,5 @@ for i in range(255):
         break
     out.append(buf[i] - prev)
     prev = buf[i]
-print(f"B={B} Ht={Ht} nlev={nl}: total {prev - t0} cycles over {len(out)} phases")
+print(f"multi={ntab > 1} B={B} Ht={Ht} nlev={nl}: total {prev - t0} cycles over {len(out)} phases")
 print(" ".join(str(x) for x in out))
