@@ -200,6 +200,9 @@ size_t fea_transfer_weight_grad_ws_bytes_f64(int C, int B, int Hc, int Wc);
  * (2) Framed multigrid-level ops (MultigridSolver), H x W grids (H, W >= 3; the intergrid ops need
  *     odd H and W: the coarse grid is (H+1)/2 x (W+1)/2, fine nodes (2I, 2J) on coarse (I, J)).
  *     `pid`/`pidc` are framed uint8 maps with the same ld (in bytes) as the T fields.
+ *     Two-material stencils (ntab > 1): each node's stiffness weights are read from its own pattern's row with
+ *     mirrored taps (ktab[p(i)][8-t] for tap t), which equals KNet's ktab[p(i+t)][t] (FEANet/model.py:22-30) bit for
+ *     bit when K is a symmetric FE stiffness (stencil_table(); feanet_amd.mesh_setup.stencil_mirror_mismatches).
  * ------------------------------------------------------------------------- */
 
 /* contiguous [B,1,H,W] -> framed, applying u*geo + bc (src NULL: u = 0; geo NULL: the square geometry,
