@@ -358,14 +358,34 @@ def cpu_baseline(n, seconds_budget=16.0):
                                      "sample": f"{kn} V-cycles (median {tn:.2f} s) by oracle/feanet_oracle.py"}}
 
 
-def single_gpu_same_grid(m, n, T, B, steps, ms_dd):
-    """The single-GPU MultigridSolver on the decomposed run's global grid ((m+1) x (n+1), same seeded rhs),
-    timed like the main line (warm-up calls, then one vcycle(steps) between synchronisations)."""
-    from feanet_amd.solver import MultigridSolver
+def dd_problem_kw(args):
+    """Solver keywords of the decomposed run's problem: Poisson, or the two-material problem with the linear or the
+    learned (BASELINE C3) transfers — the same for DDSolver and for the single-GPU solver it is checked against."""
+    if args.problem != "interface":
+        return {}
+    kw = {"problem": "interface"}
+    if args.transfer == "learned":
+        w = np.load(os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
+        kw.update(R=w["R"][0], P=w["P"][:, 0], w=w["w"])
+    return kw
+
+
+def dd_rhs(args, m, n, T, B):
+    """The decomposed run's global right-hand side (every rank draws the same one and keeps its block): seeded randn
+    f for Poisson, the nodal source F = ones (FNet applied) for the two-material problem."""
+    if args.problem == "interface":
+        return {"F": torch.ones(B, 1, m + 1, n + 1, device="cuda", dtype=T)}
     g = torch.Generator(device="cuda")
     g.manual_seed(1234)
-    s = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B)
-    s.set_rhs(f=torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g))
+    return {"f": torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g)}
+
+
+def single_gpu_same_grid(args, m, n, T, B, steps, ms_dd):
+    """The single-GPU MultigridSolver on the decomposed run's global grid ((m+1) x (n+1), same rhs),
+    timed like the main line (warm-up calls, then one vcycle(steps) between synchronisations)."""
+    from feanet_amd.solver import MultigridSolver
+    s = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B, **dd_problem_kw(args))
+    s.set_rhs(**dd_rhs(args, m, n, T, B))
     s.load()
     for _ in range(6):
         s.vcycle(steps)
@@ -378,21 +398,17 @@ def single_gpu_same_grid(m, n, T, B, steps, ms_dd):
     torch.cuda.empty_cache()
     return {"ms_per_step": t * 1e3, "value": B * (m + 1) * (n + 1) / t, "unit": "DoF-updates/s",
             "speedup_of_this_line": t * 1e3 / ms_dd,
-            "workload": f"{m + 1}x{n + 1} poisson V-cycle on one GPU (MultigridSolver, no decomposition), rank 0"}
+            "workload": f"{m + 1}x{n + 1} {args.problem} V-cycle on one GPU (MultigridSolver, no decomposition), rank 0"}
 
 
-def dd_reference_block(owned, m, n, T, B, cycles=3):
+def dd_reference_block(args, owned, m, n, T, B, cycles=3):
     """The single-GPU MultigridSolver's iterate after `cycles` V-cycles from zero on the decomposed run's global grid
-    and seeded rhs, cut to this rank's owned block ((y0, y1), (x0, x1)); run on the rank's own GPU, no
+    and rhs, cut to this rank's owned block ((y0, y1), (x0, x1)); run on the rank's own GPU, no
     communication.  The reference point of every dd mode's parity check."""
     from feanet_amd.solver import MultigridSolver
     (y0, y1), (x0, x1) = owned
-    g = torch.Generator(device="cuda")
-    g.manual_seed(1234)
-    f = torch.randn(B, 1, m + 1, n + 1, device="cuda", dtype=T, generator=g)
-    ref = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B)
-    ref.set_rhs(f=f)
-    del f
+    ref = MultigridSolver(n, rows=None if m == n else m, dtype=T, batch=B, **dd_problem_kw(args))
+    ref.set_rhs(**dd_rhs(args, m, n, T, B))
     ref.load()
     ref.vcycle(cycles)
     exp = ref.solution()[:, :, y0:y1, x0:x1].clone()
@@ -636,9 +652,10 @@ def run_dd(args, ws, rank, T, B, guard, emit):
         modes = [md for md in modes if not md[1]]
     if not modes:
         raise SystemExit(f"bench: no dd mode selected from {args.dd_modes!r} for backend {args.backend}")
-    g = torch.Generator(device="cuda")
-    g.manual_seed(1234)  # one global problem: every rank draws the same rhs and keeps its block
-    f = torch.randn(B, 1, m + 1, nc + 1, device="cuda", dtype=T, generator=g)
+    if args.problem == "interface" and m != nc:
+        raise SystemExit(f"bench: the two-material problem is defined on the square; the dd grid is {m}x{nc}")
+    rhs = dd_rhs(args, m, nc, T, B)  # one global problem: every rank draws the same rhs and keeps its block
+    pkw = dd_problem_kw(args)
     dof = B * (m + 1) * (nc + 1)
     rec, exp, results = None, None, []
 
@@ -656,8 +673,8 @@ def run_dd(args, ws, rank, T, B, guard, emit):
         try:
             with guard.phase(f"dd mode {name}", args.mode_timeout, None if i == 0 else expire):
                 s = DDSolver(nc, m, rank, ws, comm=TorchComm(capture=cap), agglomerate=args.agglomerate, dtype=T,
-                             batch=B, grid=grid, overlap_l0=ov, split_join=sj)
-                s.set_rhs(f)
+                             batch=B, grid=grid, overlap_l0=ov, split_join=sj, **pkw)
+                s.set_rhs(**rhs)
                 s.load()
                 conv = contraction(s) if i == 0 else None
                 t, warm = time_steps(s, args.steps, args.warmup, ws)
@@ -665,7 +682,7 @@ def run_dd(args, ws, rank, T, B, guard, emit):
                 par = None
                 if not args.no_dd_parity:
                     if exp is None:
-                        exp = dd_reference_block(s.owned_block()[:2], m, nc, T, B)
+                        exp = dd_reference_block(args, s.owned_block()[:2], m, nc, T, B)
                     par = dd_parity(s, exp, m, nc, ws)
                     if cap:
                         captured = captured and bool(s._capture_ok)
@@ -689,16 +706,19 @@ def run_dd(args, ws, rank, T, B, guard, emit):
             fine = time_fine_kernels(s.local, args.kernel_reps)
             roof, ns, fl = roofline_record(fine, s.local, args, ws=ws)
             p0, q0 = s.parts[0], s.cparts[0]
-            workload = (f"{m + 1}x{nc + 1} poisson {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
+            workload = (f"{m + 1}x{nc + 1} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
                         f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
                         f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
                         + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))
             parallelism = (f"dd{ws}: {grid[0]}x{grid[1]} 2-D blocks, RCCL halo exchange (one phase, packed, depths "
                            f"{s.depths}) once per V-cycle + all-gather of level {s.Ld}, redundant coarse solve")
-            rec = base_record(args, r["value"], ms, ws, warm, workload, "dd", parallelism, "randn", s.L, B)
+            rec = base_record(args, r["value"], ms, ws, warm, workload, "dd", parallelism,
+                              "ones" if args.problem == "interface" else "randn", s.L, B)
             rec.update({"roofline": roof, "north_star_kernel": ns, "fine_level_kernels": fl,
                         "vcycle_hbm_gbps_algorithmic": None, "vcycle_algorithmic_bytes": None,
                         "residual_contraction_per_cycle": conv, "dd_modes": results, "cpu_baseline": None})
+            if args.problem == "interface":
+                rec["config"]["transfer"] = ("learned ratio R/P/w" if "R" in pkw else "linear")
             if ws > 1:
                 # the same global grid on ONE GPU (rank 0; the others wait at the barrier): the strong-scaling base
                 # point of this line, so speed-up and efficiency follow from the line itself
@@ -706,7 +726,7 @@ def run_dd(args, ws, rank, T, B, guard, emit):
                 torch.cuda.empty_cache()
                 with guard.phase("single-GPU base point (rank 0) + barrier", args.mode_timeout):
                     if rank == 0:
-                        rec["single_gpu_same_grid"] = single_gpu_same_grid(m, nc, T, B, args.steps, ms)
+                        rec["single_gpu_same_grid"] = single_gpu_same_grid(args, m, nc, T, B, args.steps, ms)
                     barrier(ws)
         ok = [x for x in results if x["status"] == "ok" and (x["dd_parity"] is None or x["dd_parity"]["bitwise_equal"])]
         best = min(ok, key=lambda x: x["ms_per_step"]) if ok else results[0]
@@ -865,8 +885,6 @@ def main():
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     mode = args.mode or ("dd" if ws > 1 else "single")
-    if mode == "dd" and args.problem != "poisson":
-        raise SystemExit("bench: the domain-decomposed path runs the Poisson problem")
     ws, rank = dist_init(force=(mode == "dd"), backend=args.backend, timeout_s=args.dist_timeout)
     guard = PhaseGuard(rank)
     T = torch.float64 if args.dtype == "f64" else torch.float32

@@ -37,10 +37,9 @@ import os
 
 import torch
 
-from . import _lib
+from . import _lib, mesh_setup as ms, ops
 from .schedule import pair_prolongations, pair_restrictions, vcycle_schedule
 from .solver import MultigridSolver
-
 
 
 def global_levels(m, n):
@@ -449,7 +448,8 @@ class DDSolver:
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
                  batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5,
-                 split_join=False, fold_gather=True):
+                 split_join=False, fold_gather=True, problem="poisson", prop=(1, 20), shape=0, size=2.0, R=None,
+                 P=None, w=(1.0, 1.0)):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
         self.graph_min = graph_min
@@ -469,12 +469,28 @@ class DDSolver:
         self.device = torch.device(device if device is not None else "cuda")
         self.nu1, self.nu2, self.fuse = nu1, nu2, fuse
         p0, q0 = self.parts[0], self.cparts[0]
+        self.problem = problem
+        self.mass = ms.mass_stencil(size / n)  # FNet of the global grid (the local solvers' own mesh size differs)
+        kw = {}
+        local_maps = None
+        if problem == "interface":
+            # MeshCenterInterface (FEANet/mesh.py:4-120) on the global square: every rank's levels take their window
+            # of the global level's pattern map; the agglomerated coarse solver builds the global maps of its levels
+            if rows != n:
+                raise ValueError("DDSolver: the two-material problem is defined on the square only")
+            kw = dict(problem="interface", prop=prop, shape=shape, size=size, R=R, P=P, w=w)
+            local_maps = []
+            for l, (lp, lq) in enumerate(zip(self.parts, self.cparts)):
+                gmap = ms.interface_pattern_map((n >> l) + 1, shape, size)
+                local_maps.append(gmap[lp.gr0:lp.gr0 + lp.Hloc, lq.gr0:lq.gr0 + lq.Hloc])
+        elif problem != "poisson":
+            raise ValueError(f"DDSolver: unknown problem {problem!r}")
         self.local = MultigridSolver(q0.Hloc - 1, rows=p0.Hloc - 1, levels=self.Ld + 1, dtype=dtype,
                                      device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse, coarse_tail=False,
-                                     graph=False)
+                                     graph=False, pid_maps=local_maps, **kw)
         self.coarse = MultigridSolver(n >> self.Ld, rows=rows >> self.Ld, levels=self.L - self.Ld, dtype=dtype,
                                       device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse,
-                                      coarse_tail=True, graph=False, zero_start=True)
+                                      coarse_tail=True, graph=False, zero_start=True, **kw)
         for l, (lp, lq) in enumerate(zip(self.parts, self.cparts)):
             Lv = self.local.levels[l]
             assert Lv.H == lp.Hloc and Lv.W == lq.Hloc, (l, Lv.H, Lv.W, lp, lq)
@@ -512,8 +528,14 @@ class DDSolver:
             x = x.expand(self.B, 1, self.H, self.W)
         return x[:, :, p0.gr0:p0.gr0 + p0.Hloc, q0.gr0:q0.gr0 + q0.Hloc].contiguous()
 
-    def set_rhs(self, f):
-        """Assembled right-hand side of the GLOBAL problem, [B, 1, H, W] (any device)."""
+    def set_rhs(self, f=None, F=None):
+        """Assembled right-hand side of the GLOBAL problem f, [B, 1, H, W] (any device), or its nodal source F
+        (FNet applied to the global field first, as MultigridSolver.set_rhs(F=...))."""
+        if (f is None) == (F is None):
+            raise ValueError("DDSolver.set_rhs: give exactly one of f (assembled) or F (source)")
+        if F is not None:
+            F = F.to(self.device, self.dtype).reshape(-1, 1, self.H, self.W)
+            f = ops.conv3x3(F, torch.from_numpy(self.mass))
         self.local._pack(self._local_rows(f), self.local.levels[0].f, reset=False)
 
     def load(self, u0=None, bc=None):
@@ -559,8 +581,8 @@ class DDSolver:
         L0 = self.local.levels[0]
         p0, q0 = self.parts[0], self.cparts[0]
         loc = self.local
-        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(), None,
-                  loc.ktab.data_ptr(), loc.ntab, loc.norm_out.data_ptr(), loc.ws.data_ptr(), *L0.geom(),
+        _lib.call("mg_residual_norm", self.dtype, L0.buf(self._state).data_ptr(), L0.f.data_ptr(),
+                  None if L0.pid is None else L0.pid.data_ptr(), loc.ktab.data_ptr(), loc.ntab, loc.norm_out.data_ptr(), loc.ws.data_ptr(), *L0.geom(),
                   p0.lo, p0.hi, q0.lo, q0.hi, torch.cuda.current_stream(self.device).cuda_stream)
         return loc.norm_out * loc.norm_out
 
@@ -1299,9 +1321,9 @@ class LocalGroup:
     def __init__(self, n, rows, world, **kw):
         self.ranks = [DDSolver(n, rows, r, world, comm=None, **kw) for r in range(world)]  # kw: grid=(Pr, Pc), ...
 
-    def set_rhs(self, f):
+    def set_rhs(self, f=None, F=None):
         for s in self.ranks:
-            s.set_rhs(f)
+            s.set_rhs(f, F)
 
     def load(self, u0=None, bc=None):
         for s in self.ranks:

@@ -124,6 +124,9 @@ class MultigridSolver:
             launch (fea_mg_hmid_down / fea_mg_hmid_up, bitwise the fused per-level HJac kernels).
         pair_levels: two consecutive zero-guess restrictions, and two recomputed-iterate prolongations, left
             to single-level launches run as one each (fea_mg_zero_restrict2 / fea_mg_prolong2, bitwise the two).
+        pid_maps: two-material problem only — explicit per-level pattern maps ([H_l, W_l] uint8, one per level)
+            instead of the MeshCenterInterface maps of the square: a domain-decomposed rank's window of the
+            global level maps (feanet_amd.dd.DDSolver(problem="interface")); allows a rectangular window.
     """
 
     MID_NODES = 20000     # levels with <= this many nodes (B*H*W) may go to the LDS-tile multi-level launches (groups
@@ -149,7 +152,7 @@ class MultigridSolver:
     def __init__(self, n, levels=None, problem="poisson", dtype=torch.float64, device=None, batch=1,
                  omega=2.0 / 3.0, size=2.0, prop=(1, 20), shape=0, R=None, P=None, w=(1.0, 1.0),
                  nu1=1, nu2=1, compat=None, graph=True, coarse_tail=True, fuse=True, rows=None, zero_start=False,
-                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_levels=True):
+                 smoother="jac", hnet=None, join_cycles=True, mid=True, pair_levels=True, pid_maps=None):
         m = n if rows is None else int(rows)
         if rows is None and (n < 2 or (n & (n - 1)) != 0):
             raise ValueError(f"MultigridSolver: n={n} must be a power of two >= 2")
@@ -201,8 +204,12 @@ class MultigridSolver:
         multi = problem == "interface"
         if problem not in ("poisson", "interface"):
             raise ValueError(f"MultigridSolver: unknown problem {problem!r}")
-        if multi and m != n:
+        if multi and m != n and pid_maps is None:
             raise ValueError("MultigridSolver: the two-material problem is defined on the square only")
+        if pid_maps is not None:  # explicit per-level maps (a domain-decomposed rank's window of the global maps)
+            if not multi:
+                raise ValueError("MultigridSolver: pid_maps is for the two-material problem")
+            pid_maps = [np.ascontiguousarray(p, np.uint8) for p in pid_maps]
         ktab = ms.stencil_table(prop if multi else None)
         self.ntab = ktab.shape[0]
         lin = ms.linear_transfer_kernel() / np.float32(4.0)
@@ -231,9 +238,18 @@ class MultigridSolver:
         self.levels = []
         for l in range(self.L):
             nl, ml = n >> l, m >> l
+            if pid_maps is not None:
+                if pid_maps[l].shape != (ml + 1, nl + 1):
+                    raise ValueError(f"MultigridSolver: pid_maps[{l}] is {pid_maps[l].shape}, level {l} is "
+                                     f"{(ml + 1, nl + 1)}")
+                self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid_np=pid_maps[l]))
+                continue
             # two-material pattern maps: built on the device (setup_ops.hip), bit-identical to the host
             self.levels.append(_Level(ml, nl, self.B, dtype, dev, pid_shape=(shape, size) if multi else None))
-        self.fine_pid = ms.interface_pattern_map_device(n + 1, shape, size, device=dev) if multi else None
+        if pid_maps is not None:
+            self.fine_pid = torch.from_numpy(pid_maps[0]).to(dev)
+        else:
+            self.fine_pid = ms.interface_pattern_map_device(n + 1, shape, size, device=dev) if multi else None
         if multi:  # the framed kernels read each node's stiffness row from its own pattern (K symmetric; checked)
             for Lv in self.levels:
                 off = 128 // (4 if dtype == torch.float32 else 8) - 1
@@ -262,8 +278,8 @@ class MultigridSolver:
                     break
         t_from = self.tail_from if self.tail_from is not None else self.hjac_tail_from
         if t_from is not None and multi:
-            maps = [ms.interface_pattern_map(self.levels[l].N, shape, size).reshape(-1)
-                    for l in range(t_from, self.L)]
+            maps = [pid_maps[l].reshape(-1) if pid_maps is not None else
+                    ms.interface_pattern_map(self.levels[l].N, shape, size).reshape(-1) for l in range(t_from, self.L)]
             self.tail_pid = torch.from_numpy(np.concatenate(maps)).to(dev)
         else:
             self.tail_pid = None

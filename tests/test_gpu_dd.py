@@ -24,9 +24,9 @@ def _global_problem(m, n, B, seed=0):
     return f, u0, bc * (1 - inner)
 
 
-def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1)):
+def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1), problem="poisson"):
     from feanet_amd.solver import MultigridSolver
-    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1])
+    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1], problem=problem)
     s.set_boundary(bc)
     s.set_rhs(f=f)
     s.load(u0)
@@ -76,6 +76,44 @@ def test_dd_local_group_bitwise(m, n, P, Ld, B, graph, nu, grid):
     s.vcycle(2)
     grp.vcycle(2)
     assert torch.equal(grp.solution(), s.solution())
+
+
+def _learned_ratio():
+    here = os.path.dirname(os.path.abspath(__file__))
+    w = np.load(os.path.join(here, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
+    return dict(R=w["R"][0], P=w["P"][:, 0], w=w["w"])
+
+
+@pytest.mark.parametrize("n,P,Ld,B,nu,grid,learned", [(512, 4, 2, 1, (1, 1), (2, 2), False),
+                                                      (512, 2, 2, 2, (1, 1), None, True),
+                                                      (1024, 8, 3, 1, (1, 1), (4, 2), True),
+                                                      (1024, 4, 3, 1, (2, 2), (2, 2), False),
+                                                      (768, 6, 2, 1, (1, 1), (3, 2), True)])
+def test_dd_interface_local_group_bitwise(n, P, Ld, B, nu, grid, learned):
+    """The two-material problem (MeshCenterInterface, FEANet/mesh.py:4-120) decomposed: every rank's levels carry
+    their window of the global level's pattern map (DDSolver(problem='interface') -> MultigridSolver(pid_maps=...)),
+    the agglomerated coarse solver the global maps of its levels; linear and learned (BASELINE C3) transfers.  Owned
+    nodes bitwise the single-GPU two-material V-cycle, with the rhs given as the nodal source F (FNet of the global
+    mesh applied before the split)."""
+    from feanet_amd.dd import LocalGroup
+    from feanet_amd.solver import MultigridSolver
+    kw = _learned_ratio() if learned else {}
+    g = torch.Generator(device="cuda")
+    g.manual_seed(21)
+    F = torch.rand(B, 1, n + 1, n + 1, device="cuda", dtype=torch.float64, generator=g)
+    u0 = torch.randn(B, 1, n + 1, n + 1, device="cuda", dtype=torch.float64, generator=g)
+    s = MultigridSolver(n, rows=n, problem="interface", dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1], **kw)
+    s.set_rhs(F=F)
+    s.load(u0)
+    grp = LocalGroup(n, n, P, agglomerate=Ld, batch=B, nu1=nu[0], nu2=nu[1], grid=grid, problem="interface", **kw)
+    grp.set_rhs(F=F)
+    grp.load(u0)
+    for k in (1, 1, 3, 2):
+        s.vcycle(k)
+        grp.vcycle(k)
+        got = grp.solution()
+        assert torch.equal(got, s.solution()), f"{k}: max diff {(got - s.solution()).abs().max().item():.3e}"
+    torch.testing.assert_close(grp.residual_norm(), s.residual_norm(), rtol=1e-12, atol=0)
 
 
 def _free_port():
@@ -222,8 +260,10 @@ class _FakeDist:
 
 @pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("overlap_l0", [False, True])
-@pytest.mark.parametrize("m,n,P,Ld,grid", [(512, 256, 2, 2, (2, 1)), (512, 512, 4, 2, (2, 2)), (512, 1024, 8, 2, (4, 2))])
-def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph, monkeypatch):
+@pytest.mark.parametrize("m,n,P,Ld,grid,problem", [(512, 256, 2, 2, (2, 1), "poisson"), (512, 512, 4, 2, (2, 2), "poisson"),
+                                                   (512, 1024, 8, 2, (4, 2), "poisson"),
+                                                   (512, 512, 8, 2, (4, 2), "interface")])
+def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, problem, overlap_l0, graph, monkeypatch):
     """TorchComm's RCCL branch (device views sent directly when contiguous; otherwise the one-phase packed
     batch with its pack inside the kernel segment, one message per neighbour including the diagonal ones;
     with overlap_l0 the deferred level-0 exchange; all_gather_into_tensor into the coarse f, all_reduce of
@@ -235,7 +275,7 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph, m
     from feanet_amd.dd import DDSolver, TorchComm
     f, u0, bc = _global_problem(m, n, 1, seed=3)
     calls = (1, 1, 1, 2, 2, 2) if graph else (1, 2)
-    _, ref = _single(m, n, 1, f, u0, bc, sum(calls))
+    _, ref = _single(m, n, 1, f, u0, bc, sum(calls), problem=problem)
     torch.cuda.synchronize()
     fake = _FakeDist(P)
     out, errs = {}, []
@@ -258,7 +298,7 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, overlap_l0, graph, m
             # the legacy default stream, which would synchronise with (and break) another rank's graph capture
             with torch.cuda.stream(torch.cuda.Stream()):
                 s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=graph, overlap_l0=overlap_l0,
-                             **({"graph_min": 1} if graph else {}))
+                             problem=problem, **({"graph_min": 1} if graph else {}))
                 s.set_rhs(f)
                 s.load(u0, bc)
                 for k in calls:  # vcycle(2): joined cycles, the deferred level-0 halo finish
