@@ -360,10 +360,15 @@ def cpu_baseline(n, seconds_budget=16.0):
 
 def dd_problem_kw(args):
     """Solver keywords of the decomposed run's problem: Poisson, or the two-material problem with the linear or the
-    learned (BASELINE C3) transfers — the same for DDSolver and for the single-GPU solver it is checked against."""
+    learned (BASELINE C3) transfers; weighted Jacobi or the learned smoother (--smoother hjac) — the same for DDSolver
+    and for the single-GPU solver it is checked against."""
+    kw = {}
+    if args.smoother == "hjac":  # the learned smoother (M-FEANet-mg_test.ipynb HRelax, the bench's HNet weights)
+        w = np.load(os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
+        kw.update(smoother="hjac", hnet=np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)]))
     if args.problem != "interface":
-        return {}
-    kw = {"problem": "interface"}
+        return kw
+    kw["problem"] = "interface"
     if args.transfer == "learned":
         w = np.load(os.path.join(ROOT, "multigrid-feanet_amd", "feanet_amd", "weights", "multigrid_interface_ratio.npz"))
         kw.update(R=w["R"][0], P=w["P"][:, 0], w=w["w"])
@@ -704,9 +709,13 @@ def run_dd(args, ws, rank, T, B, guard, emit):
         results.append(r)
         if i == 0:
             fine = time_fine_kernels(s.local, args.kernel_reps)
-            roof, ns, fl = roofline_record(fine, s.local, args, ws=ws)
+            # the learned smoother joins no cycles: its dominant kernel is the slowest finest-level launch of the
+            # local cycle (timed in the rank's local V-cycle plan, which has the same finest-level launches)
+            dom = time_fine_launch_in_cycle(s.local) if args.smoother == "hjac" else None
+            roof, ns, fl = roofline_record(fine, s.local, args, dom=dom, ws=ws)
             p0, q0 = s.parts[0], s.cparts[0]
-            workload = (f"{m + 1}x{nc + 1} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1), domain-decomposed into "
+            workload = (f"{m + 1}x{nc + 1} {args.problem} {args.dtype} V-cycle, L={s.L}, V(1,1)"
+                        f"{' (learned HRelax smoother)' if args.smoother == 'hjac' else ''}, domain-decomposed into "
                         f"{grid[0]}x{grid[1]} blocks of {p0.e - p0.s} x {q0.e - q0.s} owned nodes (+{s.part.ghost(0)} "
                         f"ghost lines per side), levels >= {s.Ld} agglomerated, batch {B}"
                         + ("" if args.weak else " (BASELINE config C4 when 8193^2 over 8 GPUs)"))

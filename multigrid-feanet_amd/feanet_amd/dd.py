@@ -38,7 +38,7 @@ import os
 import torch
 
 from . import _lib, mesh_setup as ms, ops
-from .schedule import pair_prolongations, pair_restrictions, vcycle_schedule
+from .schedule import hjac_schedule, pair_prolongations, pair_restrictions, vcycle_schedule
 from .solver import MultigridSolver
 
 
@@ -154,19 +154,23 @@ def default_grid(P):
     return best
 
 
-def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a", depths=(4, 4)):
+def dd_schedule(Ld, nu1=1, nu2=1, fuse=True, start="a", depths=(4, 4), smoother="jac"):
     """The distributed part of one (unjoined) V-cycle: kernel steps of feanet_amd.schedule plus
-    ("exchange", l, buf, depth), ("gather",), ("coarse",), ("scatter", dst).  depths = (D0, D1)."""
+    ("exchange", l, buf, depth), ("gather",), ("coarse",), ("scatter", dst).  depths = (D0, D1).
+    smoother="hjac": the learned smoother's V-cycle (hjac_schedule), its levels >= Ld agglomerated the same way."""
     D0, D1 = depths
-    steps, end = vcycle_schedule(Ld + 1, nu1, nu2, None, start, tail_from=Ld, fuse=fuse)
+    if smoother == "hjac":
+        steps, end = hjac_schedule(Ld + 1, nu1, nu2, start, tail_from=Ld, fuse=fuse)
+    else:
+        steps, end = vcycle_schedule(Ld + 1, nu1, nu2, None, start, tail_from=Ld, fuse=fuse)
     out = []
     for i, st in enumerate(steps):
         kind, l = st[0], st[1]
-        if kind == "coarse_tail":
+        if kind in ("coarse_tail", "hjac_tail"):
             out += [("gather",), ("coarse",), ("scatter", st[2])]
             continue
         out.append(st)
-        if kind in ("resid_restrict", "sweep_restrict") and l == 0 and Ld >= 2:
+        if kind in ("resid_restrict", "sweep_restrict", "hsweep_restrict") and l == 0 and Ld >= 2:
             out.append(("exchange", 1, "f", D1))
     out.append(("exchange", 0, end, D0))
     return out, end
@@ -177,12 +181,13 @@ def _restricted(r):
     return (r - 1) // 2 if r >= 1 else -1
 
 
-def simulate_validity(program, Ld, ghost, init=None):
+def simulate_validity(program, Ld, ghost, init=None, nl=0):
     """Row validity along a list of dd steps: for every (level, buffer) the number of ghost rows past
     the owned rows that hold the single-grid values (owned rows exact iff >= 0).  Buffers start as in
     `init` (default: fully valid, as after load()); f_0 is static (fully valid).  Returns False as soon
     as a kernel would write a wrong owned row, else the final validity map.  Steps may also be
-    ("join", pre, ec_name)."""
+    ("join", pre, ec_name).  nl: HNet conv layers of the learned smoother's steps (HRelax: the Jacobi
+    sweep j = J(u) loses one line, each of the nl 3x3 convolutions of (j - u) * g one more)."""
     INF = 1 << 30
     v = dict(init or {})
     g = [ghost(l) for l in range(Ld + 1)]
@@ -217,6 +222,18 @@ def simulate_validity(program, Ld, ghost, init=None):
             l = st[1]
             if not put(l, st[3], min(get(l, st[2]) - 1, get(l, "f"))):
                 return False
+        elif k in ("hsweep", "hsweep_restrict"):
+            l, src, dst = st[1], st[2], st[3]
+            it = min(get(l, src) - 1, get(l, "f")) - nl
+            if not put(l, dst, it):
+                return False
+            if k == "hsweep_restrict" and not put(l + 1, "f", _restricted(min(it - 1, get(l, "f")))):
+                return False
+        elif k == "prolong_hsweep":
+            l, src, ec, dst = st[1:5]
+            x = min(get(l, src), 2 * get(l + 1, ec) - 1)
+            if not put(l, dst, min(x - 1, get(l, "f")) - nl):
+                return False
         elif k in ("resid_restrict", "sweep_restrict"):
             l, src, dst = st[1], st[2], st[3]
             if k == "sweep_restrict" or src is None:
@@ -245,13 +262,13 @@ def simulate_validity(program, Ld, ghost, init=None):
     return v
 
 
-def exchange_depths(Ld, ghost, nu1=1, nu2=1, fuse=True, joined=True):
+def exchange_depths(Ld, ghost, nu1=1, nu2=1, fuse=True, joined=True, smoother="jac", nl=0):
     """Smallest (D0, D1) (by bytes: D1 rows are half as wide) keeping the owned rows exact in every
     program DDSolver runs.  Across program boundaries only the finest iterate carries over, and every
     program ends by exchanging it (D0 rows): so checking each program once from the weakest start
     state (finest iterates valid to exactly D0) covers any sequence of them (induction)."""
     def programs(D):
-        out = [dd_schedule(Ld, nu1, nu2, fuse, "a", D)[0]]
+        out = [dd_schedule(Ld, nu1, nu2, fuse, "a", D, smoother)[0]]
         if joined:
             for njoin in (0, 1, 2):
                 seq, s = [], "a"
@@ -263,7 +280,7 @@ def exchange_depths(Ld, ghost, nu1=1, nu2=1, fuse=True, joined=True):
 
     def ok(D0, D1):
         init = {(0, "a"): D0, (0, "b"): D0}
-        return all(simulate_validity(p, Ld, ghost, init) for p in programs((D0, D1)))
+        return all(simulate_validity(p, Ld, ghost, init, nl) for p in programs((D0, D1)))
 
     best = None
     top1 = ghost(1) if Ld >= 2 else 1
@@ -314,12 +331,12 @@ def _joined_chunk_steps(Ld, nu1, nu2, fuse, kind, s, D):
     return mid + [ps, ("exchange", 0, ps[4], D0)], other(s)
 
 
-def _joined(nu1, nu2, fuse):
+def _joined(nu1, nu2, fuse, smoother="jac"):
     """Whether the local solver joins consecutive cycles (MultigridSolver._joinable for a DD slab)."""
-    return nu1 == 1 and nu2 == 1 and fuse
+    return nu1 == 1 and nu2 == 1 and fuse and smoother == "jac"
 
 
-def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None):
+def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None, smoother="jac", nl=0):
     """The Pr x Pc partition (default P x 1: row slabs) with the fewest ghost lines (G at level Ld,
     doubling per finer level) for which exchange depths exist, and those depths.  Ghost lines are
     redundant work."""
@@ -334,7 +351,8 @@ def _partition_for(m, n, P, Ld, nu1=1, nu2=1, fuse=True, grid=None):
             err = e
             break
         try:
-            return part, exchange_depths(Ld, part.ghost, nu1, nu2, fuse, joined=_joined(nu1, nu2, fuse))
+            return part, exchange_depths(Ld, part.ghost, nu1, nu2, fuse, joined=_joined(nu1, nu2, fuse, smoother),
+                                         smoother=smoother, nl=nl)
         except ValueError as e:
             err = e
     raise ValueError(f"DD: no {Pr} x {Pc} partition of a {m} x {n} grid with Ld = {Ld}: {err}")
@@ -443,13 +461,15 @@ class DDSolver:
     segment) — off by default: on one GPU (8-rank projection,
     8193^2, 4x2) the split costs 142 instead of 117 us per cycle (thin border rectangles are mostly pipeline
     fill, the interior shares the CUs with them), more than an exchange of this size takes; overlap_l0
-    overlaps the level-0 halo with the coarse levels instead; other args as MultigridSolver (Poisson).
+    overlaps the level-0 halo with the coarse levels instead; problem / prop / shape / size / R / P / w (the
+    two-material problem on the square: each rank's levels carry their window of the global pattern maps) and
+    smoother / hnet (the learned HRelax smoother, unjoined cycles) as MultigridSolver; other args as MultigridSolver.
     """
 
     def __init__(self, n, rows, rank, world, comm=None, agglomerate=None, dtype=torch.float64, device=None,
                  batch=1, nu1=1, nu2=1, fuse=True, graph=True, grid=None, overlap_l0=False, graph_min=5,
                  split_join=False, fold_gather=True, problem="poisson", prop=(1, 20), shape=0, size=2.0, R=None,
-                 P=None, w=(1.0, 1.0)):
+                 P=None, w=(1.0, 1.0), smoother="jac", hnet=None):
         self.n, self.m = n, rows
         self.overlap_l0 = overlap_l0
         self.graph_min = graph_min
@@ -462,7 +482,14 @@ class DDSolver:
                    else int(agglomerate))
         if not 1 <= self.Ld <= self.L - 1:
             raise ValueError(f"DDSolver: agglomeration level {self.Ld} outside [1, {self.L - 1}]")
-        self.part, self.depths = _partition_for(rows, n, world, self.Ld, nu1, nu2, fuse, grid=(self.Pr, self.Pc))
+        if smoother not in ("jac", "hjac"):
+            raise ValueError(f"DDSolver: unknown smoother {smoother!r}")
+        if smoother == "hjac" and hnet is None:
+            raise ValueError("DDSolver: smoother='hjac' needs the HNet weights (hnet=[nl, 3, 3])")
+        self.smoother = smoother
+        nl = 0 if hnet is None else int(torch.as_tensor(hnet).reshape(-1, 3, 3).shape[0])
+        self.part, self.depths = _partition_for(rows, n, world, self.Ld, nu1, nu2, fuse, grid=(self.Pr, self.Pc),
+                                                smoother=smoother, nl=nl)
         self.parts = [self.part.level(l, rank) for l in range(self.Ld + 1)]    # rows
         self.cparts = [self.part.clevel(l, rank) for l in range(self.Ld + 1)]  # columns
         self.dtype, self.B = dtype, batch
@@ -485,6 +512,8 @@ class DDSolver:
                 local_maps.append(gmap[lp.gr0:lp.gr0 + lp.Hloc, lq.gr0:lq.gr0 + lq.Hloc])
         elif problem != "poisson":
             raise ValueError(f"DDSolver: unknown problem {problem!r}")
+        if smoother == "hjac":  # MultiGrid(mode='hjac').Step: every relaxation one HRelax sweep
+            kw.update(smoother="hjac", hnet=hnet)
         self.local = MultigridSolver(q0.Hloc - 1, rows=p0.Hloc - 1, levels=self.Ld + 1, dtype=dtype,
                                      device=self.device, batch=batch, nu1=nu1, nu2=nu2, fuse=fuse, coarse_tail=False,
                                      graph=False, pid_maps=local_maps, **kw)
@@ -495,7 +524,7 @@ class DDSolver:
             Lv = self.local.levels[l]
             assert Lv.H == lp.Hloc and Lv.W == lq.Hloc, (l, Lv.H, Lv.W, lp, lq)
         self.coarse_plan, self.coarse_end = self.coarse._build("a")
-        assert self.joinable() == _joined(nu1, nu2, fuse)
+        assert self.joinable() == _joined(nu1, nu2, fuse, smoother)
         self.use_graph = graph
         self._capture_ok = True
         # captured cycles: the finest join split into border rectangles (run with the halo exchange on a side
@@ -508,6 +537,8 @@ class DDSolver:
         self._segs = {}
         self._graphs = {}
         self._state = "a"
+        self._raw = None  # smoother="hjac": the un-reset initial iterate the first cycle after load() reads
+        self._hjac_first = False
         self.norm_sq = torch.zeros(batch, dtype=torch.float64, device=self.device)
 
     # ------------------------------------------------------------------ data
@@ -552,6 +583,16 @@ class DDSolver:
         self.local._pack(x, L0.a, reset=False)
         self.local._pack(x, L0.b, reset=False)
         self._state = "a"
+        if self.smoother == "hjac":
+            # HRelax forms J(u) - u with the iterate the driver passed, before reset_boundary (as
+            # MultigridSolver.load): the first cycle's first level-0 sweep reads it (chunk ("first", s)); one buffer
+            # for the solver's life, so captured segments keep its address
+            raw = torch.zeros((self.B, 1, H, W), dtype=self.dtype, device=self.device) if u0 is None else \
+                u0.to(self.device, self.dtype).reshape(-1, 1, H, W).expand(self.B, 1, H, W)
+            if self._raw is None:
+                self._raw = torch.zeros_like(L0.a)
+            self.local._pack(self._local_rows(raw), self._raw, reset=False)
+            self._hjac_first = True
 
     def owned_block(self):
         """((y0, y1), (x0, x1), u[B, 1, y1-y0, x1-x0]): the current iterate on the global nodes this rank
@@ -730,17 +771,46 @@ class DDSolver:
         if key in self._segs:
             return self._segs[key]
         kind, b = key
-        if kind == "cycle":
-            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, b, self.depths)
+        if kind in ("cycle", "first"):
+            steps, end = dd_schedule(self.Ld, self.nu1, self.nu2, self.fuse, b, self.depths, self.smoother)
         else:
             steps, end = _joined_chunk_steps(self.Ld, self.nu1, self.nu2, self.fuse, kind, b, self.depths)
-        res = (self._segs_of(steps), end)
+        segs = self._segs_of(steps)
+        if kind == "first":  # the first finest-level HRelax sweep reads the un-reset iterate (load())
+            segs = self._first_sweep_raw(segs)
+        res = (segs, end)
         self._segs[key] = res
         return res
+
+    def _first_sweep_raw(self, segs):
+        """The segments with the cycle's first level-0 HRelax sweep given the un-reset iterate (its u_raw slot,
+        argument 1), as MultigridSolver._vcycles_plain does for the first cycle after load()."""
+        f0 = self.local.levels[0].f.data_ptr()
+        out, done = [], False
+        for kind, launches, lvl0 in segs:
+            if kind == "k" and not done:
+                launches = list(launches)
+                for i, (name, args) in enumerate(launches):
+                    fi = {"mg_hsweep": 2, "mg_hsweep_restrict": 2, "mg_prolong_hsweep": 3}.get(name)
+                    if fi is not None and args[fi] == f0:
+                        launches[i] = (name, (args[0], self._raw.data_ptr()) + tuple(args[2:]))
+                        done = True
+                        break
+            out.append((kind, launches, lvl0))
+        return out
 
     def program(self, k):
         """The chunks of vcycle(k) from the current state, and the end state."""
         s = self._state
+        if self._hjac_first and k >= 1:  # learned smoother, first cycle after load(): never joined
+            s1 = self.chunk(("first", s))[1]
+            keys, end = self._program_from(s1, k - 1)
+            return [("first", s)] + keys, end
+        return self._program_from(s, k)
+
+    def _program_from(self, s, k):
+        if k < 1:
+            return [], s
         if k >= 2 and self.joinable():
             keys = [("head", s)]
             pre = "b" if s == "a" else "a"
@@ -905,6 +975,8 @@ class DDSolver:
         else:
             self._run_chunks(keys, captured=False)
         self._state = end
+        if k >= 1:
+            self._hjac_first = False
 
     def _vcycle_captured(self, keys):
         """vcycle with every chunk's kernels AND communication steps captured in one HIP graph per block of up to
@@ -1359,6 +1431,8 @@ class LocalGroup:
                         s.scatter(st[1])
         for s in self.ranks:
             s._state = end
+            if k >= 1:
+                s._hjac_first = False
 
     def _exchange(self, l, name, d):
         """TorchComm.exchange_many as device copies: every receive region from its peer's matching send

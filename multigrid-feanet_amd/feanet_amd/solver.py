@@ -192,7 +192,7 @@ class MultigridSolver:
         if smoother == "hjac":
             if hnet is None:
                 raise ValueError("MultigridSolver: smoother='hjac' needs the HNet weights (hnet=[nl, 3, 3])")
-            if compat is not None or zero_start:
+            if compat is not None:
                 raise ValueError("MultigridSolver: smoother='hjac' follows MultiGrid(mode='hjac').Step only")
             hw = np.asarray(torch.as_tensor(hnet).detach().cpu().float().numpy(), np.float32).reshape(-1, 3, 3)
             if not 1 <= hw.shape[0] <= 3:
@@ -449,8 +449,8 @@ class MultigridSolver:
         """Bind the symbolic schedule (feanet_amd.schedule) to C-ABI calls with device pointers:
         list of (name, args-without-stream) for one V-cycle from buffer `start`, and the end buffer."""
         if self.smoother == "hjac":
-            steps, end = hjac_schedule(self.L, self.nu1, self.nu2, start, tail_from=self.hjac_tail_from,
-                                       fuse=self.fuse)
+            steps, end = hjac_schedule(self.L, self.nu1, self.nu2, "zero" if self.zero_start else start,
+                                       tail_from=self.hjac_tail_from, fuse=self.fuse)
             if self.mid and self.fuse:
                 steps = group_hmid(steps, self._pick_hmid())
         else:

@@ -93,6 +93,27 @@ def test_partition_grows_ghosts_when_needed():
         exchange_depths(4, Partition(4096, 4096, 8, 4, 4).ghost, 2, 2, joined=False)
 
 
+@pytest.mark.parametrize("m,n,P,Ld,nl", [(512, 512, 4, 2, 3), (1024, 1024, 8, 3, 3), (512, 512, 4, 2, 1),
+                                         (16384, 8192, 8, 4, 3)])
+def test_exchange_depths_learned_smoother(m, n, P, Ld, nl):
+    """The learned smoother's decomposed V-cycle (dd_schedule(smoother='hjac')): every HRelax sweep loses 1 + nl
+    ghost lines, so the chosen partition keeps more ghost lines than Jacobi's and the depths are minimal for the
+    unjoined program; with nl HNet layers assumed fewer than the kernels apply the same depths fail."""
+    part, (D0, D1) = _partition_for(m, n, P, Ld, smoother="hjac", nl=nl)
+    init = lambda d: {(0, "a"): d, (0, "b"): d}
+    prog = lambda D: dd_schedule(Ld, 1, 1, True, "a", D, "hjac")[0]
+    kinds = {st[0] for st in prog((D0, D1))}
+    assert {"hsweep_restrict", "prolong_hsweep", "gather", "coarse", "scatter"} <= kinds and "sweep" not in kinds
+    assert simulate_validity(prog((D0, D1)), Ld, part.ghost, init(D0), nl)
+    assert not simulate_validity(prog((D0 - 1, D1)), Ld, part.ghost, init(D0 - 1), nl)
+    if Ld >= 2 and D1 > 1:
+        assert not simulate_validity(prog((D0, D1 - 1)), Ld, part.ghost, init(D0), nl)
+    jac_part, (J0, _) = _partition_for(m, n, P, Ld)
+    assert part.G >= jac_part.G and D0 >= J0 and (nl < 3 or D0 > J0)
+    if nl > 1:
+        assert not simulate_validity(prog((D0, D1)), Ld, part.ghost, init(D0), nl + 1)
+
+
 def test_default_agglomeration():
     L = global_levels(16384, 8192)
     Ld = default_agglomeration(16384, 8192, 8, L)

@@ -24,9 +24,9 @@ def _global_problem(m, n, B, seed=0):
     return f, u0, bc * (1 - inner)
 
 
-def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1), problem="poisson"):
+def _single(m, n, B, f, u0, bc, cycles, nu=(1, 1), problem="poisson", **kw):
     from feanet_amd.solver import MultigridSolver
-    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1], problem=problem)
+    s = MultigridSolver(n, rows=m, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1], problem=problem, **kw)
     s.set_boundary(bc)
     s.set_rhs(f=f)
     s.load(u0)
@@ -114,6 +114,50 @@ def test_dd_interface_local_group_bitwise(n, P, Ld, B, nu, grid, learned):
         got = grp.solution()
         assert torch.equal(got, s.solution()), f"{k}: max diff {(got - s.solution()).abs().max().item():.3e}"
     torch.testing.assert_close(grp.residual_norm(), s.residual_norm(), rtol=1e-12, atol=0)
+
+
+def _hnet():
+    here = os.path.dirname(os.path.abspath(__file__))
+    w = np.load(os.path.join(here, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
+    return np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+
+
+@pytest.mark.parametrize("m,n,P,Ld,B,nu,grid,problem,nl", [(512, 512, 4, 2, 1, (1, 1), (2, 2), "poisson", 3),
+                                                           (1024, 512, 2, 3, 2, (1, 1), None, "poisson", 3),
+                                                           (1024, 1024, 8, 3, 1, (1, 1), (4, 2), "poisson", 3),
+                                                           (512, 512, 4, 2, 1, (2, 1), (2, 2), "poisson", 1),
+                                                           (512, 512, 4, 2, 1, (1, 1), (2, 2), "interface", 3)])
+def test_dd_hjac_local_group_bitwise(m, n, P, Ld, B, nu, grid, problem, nl):
+    """The learned smoother (MultiGrid(mode='hjac').Step of M-FEANet-mg_test.ipynb:27346-27372) decomposed: every
+    relaxation one HRelax sweep, the exchange depths from the validity simulation with each sweep losing 1 + nl
+    lines, the agglomerated coarse solve the zero-start hjac V-cycle (HJac two-level launches and LDS tail), and the
+    first cycle after load() reading the un-reset iterate.  Owned nodes bitwise the single-GPU hjac V-cycle."""
+    from feanet_amd.dd import LocalGroup
+    from feanet_amd.solver import MultigridSolver
+    hw = _hnet()[:nl]
+    f, u0, bc = _global_problem(m, n, B, seed=9)
+    s = MultigridSolver(n, rows=m, problem=problem, dtype=torch.float64, batch=B, nu1=nu[0], nu2=nu[1],
+                        smoother="hjac", hnet=hw)
+    s.set_boundary(bc)
+    s.set_rhs(f=f)
+    s.load(u0)
+    grp = LocalGroup(n, m, P, agglomerate=Ld, batch=B, nu1=nu[0], nu2=nu[1], grid=grid, problem=problem,
+                     smoother="hjac", hnet=hw)
+    grp.set_rhs(f)
+    grp.load(u0, bc)
+    for k in (1, 1, 3, 2):
+        s.vcycle(k)
+        grp.vcycle(k)
+        got = grp.solution()
+        assert torch.equal(got, s.solution()), f"{k}: max diff {(got - s.solution()).abs().max().item():.3e}"
+    torch.testing.assert_close(grp.residual_norm(), s.residual_norm(), rtol=1e-12, atol=0)
+    # a second load(): the first cycle again reads the un-reset iterate (the chunk is cached, its graph replayed)
+    s.load(u0)
+    grp.load(u0, bc)
+    for k in (1, 2):
+        s.vcycle(k)
+        grp.vcycle(k)
+    assert torch.equal(grp.solution(), s.solution())
 
 
 def _free_port():
@@ -262,7 +306,8 @@ class _FakeDist:
 @pytest.mark.parametrize("overlap_l0", [False, True])
 @pytest.mark.parametrize("m,n,P,Ld,grid,problem", [(512, 256, 2, 2, (2, 1), "poisson"), (512, 512, 4, 2, (2, 2), "poisson"),
                                                    (512, 1024, 8, 2, (4, 2), "poisson"),
-                                                   (512, 512, 8, 2, (4, 2), "interface")])
+                                                   (512, 512, 8, 2, (4, 2), "interface"),
+                                                   (512, 512, 4, 2, (2, 2), "poisson+hjac")])
 def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, problem, overlap_l0, graph, monkeypatch):
     """TorchComm's RCCL branch (device views sent directly when contiguous; otherwise the one-phase packed
     batch with its pack inside the kernel segment, one message per neighbour including the diagonal ones;
@@ -275,7 +320,9 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, problem, overlap_l0,
     from feanet_amd.dd import DDSolver, TorchComm
     f, u0, bc = _global_problem(m, n, 1, seed=3)
     calls = (1, 1, 1, 2, 2, 2) if graph else (1, 2)
-    _, ref = _single(m, n, 1, f, u0, bc, sum(calls), problem=problem)
+    problem, _, sm = problem.partition("+")
+    skw = {"smoother": "hjac", "hnet": _hnet()} if sm == "hjac" else {}
+    _, ref = _single(m, n, 1, f, u0, bc, sum(calls), problem=problem, **skw)
     torch.cuda.synchronize()
     fake = _FakeDist(P)
     out, errs = {}, []
@@ -298,7 +345,7 @@ def test_dd_torchcomm_direct_device_path(m, n, P, Ld, grid, problem, overlap_l0,
             # the legacy default stream, which would synchronise with (and break) another rank's graph capture
             with torch.cuda.stream(torch.cuda.Stream()):
                 s = DDSolver(n, m, r, P, comm=comm, agglomerate=Ld, grid=grid, graph=graph, overlap_l0=overlap_l0,
-                             problem=problem, **({"graph_min": 1} if graph else {}))
+                             problem=problem, **skw, **({"graph_min": 1} if graph else {}))
                 s.set_rhs(f)
                 s.load(u0, bc)
                 for k in calls:  # vcycle(2): joined cycles, the deferred level-0 halo finish
