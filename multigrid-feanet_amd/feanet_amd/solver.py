@@ -90,8 +90,8 @@ class MultigridSolver:
 
     Args:
         n: fine-grid intervals per edge (N = n + 1 nodes), a power of two >= 2.
-        rows: intervals in the row direction when the domain is a rectangle (Poisson only; default
-            n, the reference's square).  n and rows must be divisible by 2^(L-1).
+        rows: intervals in the row direction when the domain is a rectangle (Poisson, or the two-material
+            problem with explicit pid_maps; default n, the reference's square).  n and rows must be divisible by 2^(L-1).
         levels: number of levels L (default int(log2 n), the reference's choice; coarsest n/2^(L-1);
             for a rectangle, the most levels whose coarsest grid has >= 2 intervals each way).
         problem: "poisson" (MeshSquare, one stencil) or "interface" (MeshCenterInterface, 16
