@@ -1,7 +1,8 @@
 """CPU restatement of one rank of the domain-decomposed V-cycle (feanet_amd.dd) with the oracle's
 operators on numpy blocks and torch.distributed (gloo) for the exchanges: checks the 2-D partition
 (row slabs = 1 column block), the two-phase halo exchange, the communication schedule and the coarse
-agglomeration without a GPU.  Test infrastructure."""
+agglomeration without a GPU — for the Poisson and the two-material problem (each rank's levels carry their window
+of the global pattern maps) and for weighted Jacobi and the learned HRelax smoother.  Test infrastructure."""
 import os
 import sys
 
@@ -28,18 +29,25 @@ class OracleRank:
     [gc0, gc0 + Wloc)), kernel steps executed with oracle operators (the block's edge lines are kept,
     the framed kernels' semantics)."""
 
-    def __init__(self, m, n, P, r, Ld, f, u, nu=(1, 1), grid=None):
+    def __init__(self, m, n, P, r, Ld, f, u, nu=(1, 1), grid=None, problem="poisson", hw=None):
         from feanet_amd.dd import _partition_for, global_levels
         self.m, self.n, self.P, self.r, self.Ld = m, n, P, r, Ld
         self.Pr, self.Pc = grid if grid is not None else (P, 1)
         self.ri, self.ci = divmod(r, self.Pc)
         self.L = global_levels(m, n)
         # the partition and exchange depths DDSolver uses (the oracle runs its unjoined cycles)
-        self.part, self.depths = _partition_for(m, n, P, Ld, nu[0], nu[1], fuse=True, grid=(self.Pr, self.Pc))
+        self.hw = hw
+        self.smoother = "jac" if hw is None else "hjac"
+        self.part, self.depths = _partition_for(m, n, P, Ld, nu[0], nu[1], fuse=True, grid=(self.Pr, self.Pc),
+                                                smoother=self.smoother, nl=0 if hw is None else len(hw))
         self.parts = [self.part.level(l, r) for l in range(Ld + 1)]
         self.cparts = [self.part.clevel(l, r) for l in range(Ld + 1)]
         self.lv = [orc.Level(q.Hloc - 1, "poisson", np.float64, m=p.Hloc - 1)
                    for p, q in zip(self.parts, self.cparts)]
+        if problem == "interface":  # the window of the global level's MeshCenterInterface map (oracle mesh loops)
+            for l, (p, q, lv) in enumerate(zip(self.parts, self.cparts, self.lv)):
+                ktab, pid = orc.interface_mesh((n >> l) + 1)
+                lv.ktab, lv.pid = ktab, np.asarray(pid)[p.gr0:p.gr0 + p.Hloc, q.gr0:q.gr0 + q.Hloc]
         B = f.shape[0]
         self.B = B
         p0, q0 = self.parts[0], self.cparts[0]
@@ -52,18 +60,43 @@ class OracleRank:
         self.bufs[0]["a"] = u[blk].copy()
         self.bufs[0]["b"] = u[blk].copy()
         self.R = (orc.np.array([[1, 2, 1], [2, 4, 2], [1, 2, 1]], np.float32) / 4)[None]
+        if problem == "interface":
+            self.R = np.broadcast_to(self.R, (16, 3, 3))
         self.nu = nu
-        self.coarse = orc.OracleMultigrid(n >> Ld, "poisson", np.float64, levels=self.L - Ld, rows=m >> Ld)
+        self.coarse = orc.OracleMultigrid(n >> Ld, problem, np.float64, levels=self.L - Ld, rows=m >> Ld)
+        self.coarse.hw = hw
 
     def sweep(self, l, src, f):
         lv = self.lv[l]
         return orc.jacobi_sweep(src, f, lv.pid, lv.ktab, lv.geo, src * (1 - lv.geo))
 
+    def hrelax(self, l, src, f):
+        """HRelax on the block (M-FEANet-mg_test.ipynb:147-155) with the framed kernels' semantics: the block's
+        edge lines keep their values (J keeps them, the masked HNet correction is zero there)."""
+        j = self.sweep(l, src, f)
+        return j + orc.hnet(j - src, self.lv[l].geo, self.hw)
+
+    def restrict_into(self, l, v):
+        b, lv = self.bufs, self.lv
+        fc = orc.restrict(b[l]["f"] - lv[l].K(v), lv[l].pid, self.R)
+        keep = b[l + 1]["f"].copy()
+        keep[:, 1:-1, 1:-1] = fc[:, 1:-1, 1:-1]
+        b[l + 1]["f"] = keep
+
     def kernel(self, st):
         kind, l = st[0], st[1]
         b = self.bufs
         lv = self.lv
-        if kind == "sweep":
+        if kind in ("hsweep", "hsweep_restrict"):
+            src = b[l]["zero"] if st[2] is None else b[l][st[2]]
+            v = self.hrelax(l, src, b[l]["f"])
+            b[l][st[3]] = v
+            if kind == "hsweep_restrict":
+                self.restrict_into(l, v)
+        elif kind == "prolong_hsweep":
+            x = b[l][st[2]] + orc.prolong(b[l + 1][st[3]], lv[l + 1].pid, self.R)
+            b[l][st[4]] = self.hrelax(l, x, b[l]["f"])
+        elif kind == "sweep":
             src = b[l]["zero"] if st[2] is None else b[l][st[2]]
             b[l][st[3]] = self.sweep(l, src, b[l]["f"])
         elif kind in ("resid_restrict", "sweep_restrict"):
@@ -76,17 +109,14 @@ class OracleRank:
                     b[l][st[3]] = v
             else:
                 v = b[l][st[2]]
-            r = b[l]["f"] - lv[l].K(v)
-            fc = orc.restrict(r, lv[l].pid, self.R)
-            keep = b[l + 1]["f"].copy()
-            keep[:, 1:-1, 1:-1] = fc[:, 1:-1, 1:-1]
-            b[l + 1]["f"] = keep
+            self.restrict_into(l, v)
         elif kind == "prolong_sweep":
             # the kernel's semantics: the corrected field x enters the stencil on every node (also the
             # block's local edge lines), interior nodes are swept, edge lines keep the source values
             src = self.sweep(l, b[l]["zero"], b[l]["f"]) if st[2] == "omdf" else b[l][st[2]]
             x = src + orc.prolong(b[l + 1][st[3]], lv[l + 1].pid, self.R)
-            omd = orc.omega_over_d(lv[l].ktab, 2. / 3., np.float64)[0]
+            omd = orc.omega_over_d(lv[l].ktab, 2. / 3., np.float64)
+            omd = omd[0] if len(omd) == 1 else omd[np.asarray(lv[l].pid, np.int64)]
             swept = omd * (b[l]["f"] - lv[l].K(x)) + x
             b[l][st[4]] = np.where(lv[l].geo > 0, swept, src)
         else:
@@ -113,16 +143,19 @@ class OracleRank:
 
     def coarse_solve(self, fglob):
         """The replicated coarse sub-cycle: the oracle V-cycle of levels >= Ld from a zero guess."""
-        from feanet_amd.schedule import vcycle_schedule
+        from feanet_amd.schedule import hjac_schedule, vcycle_schedule
         from test_schedule import interpret
-        steps, end = vcycle_schedule(self.L - self.Ld, 1, 1, None, "a", None, True, top_zero=True)
+        if self.hw is not None:
+            steps, end = hjac_schedule(self.L - self.Ld, 1, 1, "zero", None, True)
+        else:
+            steps, end = vcycle_schedule(self.L - self.Ld, 1, 1, None, "a", None, True, top_zero=True)
         mg = self.coarse
         mg.w = (1.0, 1.0)
         bufs = interpret(mg, steps, np.zeros_like(fglob), fglob)
         return bufs[0][end]
 
 
-def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2, grid=None):
+def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2, grid=None, kind="poisson", hw=None):
     """Process entry: one rank of the oracle DD V-cycle over gloo; saves its owned block."""
     import torch
     import torch.distributed as dist
@@ -130,10 +163,10 @@ def run_rank(rank, world, m, n, Ld, port, outdir, cycles=2, grid=None):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     B = 2
     f, u = problem(m, n, B)
-    R = OracleRank(m, n, world, rank, Ld, f, u, grid=grid)
+    R = OracleRank(m, n, world, rank, Ld, f, u, grid=grid, problem=kind, hw=hw)
     state = "a"
     for _ in range(cycles):
-        steps, end = dd_schedule(Ld, 1, 1, True, state, R.depths)
+        steps, end = dd_schedule(Ld, 1, 1, True, state, R.depths, R.smoother)
         for st in steps:
             if st[0] == "exchange":
                 l, name, DEPTH = st[1], st[2], st[3]

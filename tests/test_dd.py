@@ -172,26 +172,43 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, m, n, Ld, port, outdir, grid):
+def _worker(rank, world, m, n, Ld, port, outdir, grid, problem, hw):
     import dd_oracle
-    dd_oracle.run_rank(rank, world, m, n, Ld, port, outdir, grid=grid)
+    dd_oracle.run_rank(rank, world, m, n, Ld, port, outdir, grid=grid, kind=problem, hw=hw)
 
 
-@pytest.mark.parametrize("m,n,P,Ld,grid", [(64, 32, 2, 2, None), (96, 32, 3, 2, None), (128, 64, 2, 3, None),
-                                           (64, 64, 4, 2, (2, 2)), (64, 128, 2, 2, (1, 2)),
-                                           (128, 96, 6, 2, (2, 3))])
-def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld, grid):
+def _hnet():
+    w = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multigrid-feanet_amd", "feanet_amd",
+                             "weights", "hnet_iso_poisson_33x33.npz"))
+    return np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])
+
+
+@pytest.mark.parametrize("m,n,P,Ld,grid,problem,hjac", [(64, 32, 2, 2, None, "poisson", False),
+                                                        (96, 32, 3, 2, None, "poisson", False),
+                                                        (128, 64, 2, 3, None, "poisson", False),
+                                                        (64, 64, 4, 2, (2, 2), "poisson", False),
+                                                        (64, 128, 2, 2, (1, 2), "poisson", False),
+                                                        (128, 96, 6, 2, (2, 3), "poisson", False),
+                                                        (64, 64, 4, 2, (2, 2), "interface", False),
+                                                        (128, 64, 2, 2, None, "poisson", True),
+                                                        (64, 64, 4, 2, (2, 2), "interface", True)])
+def test_dd_vcycle_gloo_vs_single_grid(tmp_path, m, n, P, Ld, grid, problem, hjac):
     """Row slabs and 2-D blocks (the oracle rank model exchanges x then y: corners via the diagonal neighbours) over gloo,
-    world sizes 2..6, against the oracle's single-grid V-cycle on the global grid."""
+    world sizes 2..6, against the oracle's single-grid V-cycle on the global grid; also the two-material problem
+    (windows of the global pattern maps) and the learned HRelax smoother (DDSolver's exchange depths for it)."""
     import dd_oracle
-    mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path), grid), nprocs=P, join=True)
+    hw = _hnet() if hjac else None
+    mp.spawn(_worker, args=(P, m, n, Ld, _free_port(), str(tmp_path), grid, problem, hw), nprocs=P, join=True)
     got = np.full((2, m + 1, n + 1), np.nan)
     for r in range(P):
         s, e, sc, ec = map(int, open(os.path.join(tmp_path, f"rank{r}.idx")).read().split())
         got[:, s:e, sc:ec] = np.load(os.path.join(tmp_path, f"rank{r}.npy"))
     f, u = dd_oracle.problem(m, n, 2)
     L = global_levels(m, n)
-    mg = orc.OracleMultigrid(n, "poisson", np.float64, levels=L, rows=m)
+    mg = orc.OracleMultigrid(n, problem, np.float64, levels=L, rows=None if problem == "interface" else m)
+    if hjac:  # MultiGrid(mode='hjac').Step: every sweep an HRelax
+        for lv in mg.levels:
+            lv.sweep = (lambda ll, o: (lambda v, ff: (lambda j: j + orc.hnet(j - v, ll.geo, hw))(o(v, ff))))(lv, lv.sweep)
     geo, _ = orc.square_geometry((m + 1, n + 1), np.float64)
     mg.set_boundary(geo, u * (1 - geo))
     v = u
