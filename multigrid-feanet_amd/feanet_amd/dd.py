@@ -1,6 +1,7 @@
 """Domain-decomposed V-cycle over several MI355X GPUs: 2-D blocks + halo exchange.
 
-The fine grid ((m+1) x (n+1) nodes, Poisson) is cut into a Pr x Pc grid of blocks, one per rank (one
+The fine grid ((m+1) x (n+1) nodes; Poisson, or the two-material problem on the square; weighted Jacobi or the
+learned HRelax smoother) is cut into a Pr x Pc grid of blocks, one per rank (one
 process per GPU, torch.distributed over RCCL/xGMI; rank r = ri * Pc + ci).  Row slabs are the Pc = 1
 case.  Levels 0 .. Ld-1 are distributed; the level-Ld restriction is all-gathered and the rest of the
 V-cycle (levels >= Ld of the global grid) is solved redundantly on every rank by a single-GPU
