@@ -24,12 +24,15 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("ranks,grid", [(2, None), (4, "2x2")])
-def test_bench_dd_line_parity(ranks, grid):
+@pytest.mark.parametrize("ranks,grid,extra", [(2, None, []), (4, "2x2", []),
+                                              (4, "2x2", ["--problem", "interface", "--smoother", "hjac"])])
+def test_bench_dd_line_parity(ranks, grid, extra):
+    """The N > 1 line over gloo: every mode bitwise; also the decomposed two-material problem with the learned
+    smoother (--problem interface --smoother hjac)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
            "--gpus", str(ranks), "--steps", "3", "--warmup", "1", "--backend", "gloo", "--global-n", "1024",
-           "--kernel-reps", "2"] + (["--grid", grid] if grid else [])
+           "--kernel-reps", "2"] + (["--grid", grid] if grid else []) + extra
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -54,6 +57,9 @@ def test_bench_dd_line_parity(ranks, grid):
     best = min(timed, key=lambda m: m["ms_per_step"])
     assert rec["headline_mode"] == best["mode"] and rec["ms_per_step"] == best["ms_per_step"]
     assert rec["config"]["dd_mode"]["mode"] == best["mode"]
+    if extra:
+        assert "interface" in rec["config"]["workload"] and "HRelax" in rec["config"]["workload"]
+        assert base["workload"].startswith("1025x1025 interface")
 
 
 @pytest.mark.timeout(300)
