@@ -479,8 +479,13 @@ class DDSolver:
         self.ri, self.ci = divmod(rank, self.Pc)
         self.comm = comm
         self.L = global_levels(rows, n)
-        self.Ld = (default_agglomeration(rows, n, self.Pr, self.L, Pc=self.Pc) if agglomerate is None
-                   else int(agglomerate))
+        # the learned smoother stops coarsening the distributed levels earlier: its coarse levels cost more per node
+        # (the replicated coarse sub-cycle on 257^2 takes 74 us against Jacobi's 24) while its ghost lines grow with
+        # 1 + nl lines per sweep — at 8193^2 the projection's best Ld is 3 (1025^2) at 2, 4 and 8 ranks
+        # (profiles/r06_dd_hjac/dd_projection_hjac.txt: 8 ranks 334.7 us at Ld = 3 against 382.7 at Ld = 5)
+        self.Ld = (default_agglomeration(rows, n, self.Pr, self.L, Pc=self.Pc,
+                                         max_nodes=(1 << 21) if smoother == "hjac" else None)
+                   if agglomerate is None else int(agglomerate))
         if not 1 <= self.Ld <= self.L - 1:
             raise ValueError(f"DDSolver: agglomeration level {self.Ld} outside [1, {self.L - 1}]")
         if smoother not in ("jac", "hjac"):

@@ -114,6 +114,15 @@ def test_exchange_depths_learned_smoother(m, n, P, Ld, nl):
         assert not simulate_validity(prog((D0, D1)), Ld, part.ghost, init(D0), nl + 1)
 
 
+def test_default_agglomeration_learned_smoother():
+    """DDSolver's default Ld for the learned smoother: the first level with <= 2^21 nodes (8193^2: Ld = 3, the
+    projection's best at 2, 4 and 8 ranks, profiles/r06_dd_hjac), clamped to what the partition allows."""
+    L = global_levels(8192, 8192)
+    for P, Pc in ((2, 1), (2, 2), (4, 2)):
+        assert default_agglomeration(8192, 8192, P, L, max_nodes=1 << 21, Pc=Pc) == 3
+    assert default_agglomeration(1024, 1024, 2, global_levels(1024, 1024), max_nodes=1 << 21) == 1
+
+
 def test_default_agglomeration():
     L = global_levels(16384, 8192)
     Ld = default_agglomeration(16384, 8192, 8, L)

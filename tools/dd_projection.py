@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--graph-min", type=int, default=None, help="DDSolver(graph_min=): shorter segments eager")
     ap.add_argument("--no-fold-gather", action="store_true",
                     help="DDSolver(fold_gather=False): the agglomeration's staging / placement as copy launches")
+    ap.add_argument("--smoother", default="jac", choices=["jac", "hjac"],
+                    help="hjac: the learned HRelax smoother (the bench's HNet weights) on both sides")
     ap.add_argument("--split", action="store_true",
                     help="captured cycles with the border / interior split of the finest join (DDSolver split_join)")
     args = ap.parse_args()
@@ -149,14 +151,19 @@ def main():
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
     f = torch.randn(1, 1, n + 1, n + 1, dtype=torch.float64, device="cuda", generator=g)
-    single = MultigridSolver(n, dtype=torch.float64)
+    skw = {}
+    if args.smoother == "hjac":
+        import numpy as np
+        w = np.load(os.path.join(HERE, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
+        skw = {"smoother": "hjac", "hnet": np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])}
+    single = MultigridSolver(n, dtype=torch.float64, **skw)
     single.set_rhs(f=f)
     single.load()
     t1 = time_cycles(single.vcycle, args.steps)
     print(f"single GPU {n + 1}^2: {t1 * 1e6:.1f} us per V-cycle", flush=True)
     del single
     torch.cuda.empty_cache()
-    rec = {"n": n, "single_gpu_us": t1 * 1e6, "ranks": {}}
+    rec = {"n": n, "smoother": args.smoother, "single_gpu_us": t1 * 1e6, "ranks": {}}
     L = global_levels(n, n)
     for P in (int(x) for x in args.ranks.split(",")):
         Pr, Pc = default_grid(P)
@@ -170,7 +177,7 @@ def main():
                 comm.capturable = not args.segments
                 s = DDSolver(n, n, r, P, comm=comm, agglomerate=Ld, grid=(Pr, Pc),
                              graph=not args.no_graph, split_join=args.split, fold_gather=not args.no_fold_gather,
-                             **({} if args.graph_min is None else {"graph_min": args.graph_min}))
+                             **skw, **({} if args.graph_min is None else {"graph_min": args.graph_min}))
             except ValueError as e:
                 print(f"P={P} {Pr}x{Pc} Ld={Ld}: not partitionable ({e})", flush=True)
                 continue
