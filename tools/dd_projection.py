@@ -144,6 +144,8 @@ def main():
                     help="DDSolver(fold_gather=False): the agglomeration's staging / placement as copy launches")
     ap.add_argument("--smoother", default="jac", choices=["jac", "hjac"],
                     help="hjac: the learned HRelax smoother (the bench's HNet weights) on both sides")
+    ap.add_argument("--problem", default="poisson", choices=["poisson", "interface"],
+                    help="interface: the two-material problem (linear transfers) on both sides")
     ap.add_argument("--split", action="store_true",
                     help="captured cycles with the border / interior split of the finest join (DDSolver split_join)")
     args = ap.parse_args()
@@ -151,11 +153,11 @@ def main():
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
     f = torch.randn(1, 1, n + 1, n + 1, dtype=torch.float64, device="cuda", generator=g)
-    skw = {}
+    skw = {} if args.problem == "poisson" else {"problem": "interface"}
     if args.smoother == "hjac":
         import numpy as np
         w = np.load(os.path.join(HERE, "..", "multigrid-feanet_amd", "feanet_amd", "weights", "hnet_iso_poisson_33x33.npz"))
-        skw = {"smoother": "hjac", "hnet": np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)])}
+        skw.update(smoother="hjac", hnet=np.stack([w[f"conv{i}"].reshape(3, 3) for i in range(3)]))
     single = MultigridSolver(n, dtype=torch.float64, **skw)
     single.set_rhs(f=f)
     single.load()
@@ -163,7 +165,7 @@ def main():
     print(f"single GPU {n + 1}^2: {t1 * 1e6:.1f} us per V-cycle", flush=True)
     del single
     torch.cuda.empty_cache()
-    rec = {"n": n, "smoother": args.smoother, "single_gpu_us": t1 * 1e6, "ranks": {}}
+    rec = {"n": n, "smoother": args.smoother, "problem": args.problem, "single_gpu_us": t1 * 1e6, "ranks": {}}
     L = global_levels(n, n)
     for P in (int(x) for x in args.ranks.split(",")):
         Pr, Pc = default_grid(P)
